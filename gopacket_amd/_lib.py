@@ -1,0 +1,75 @@
+"""ctypes binding of the in-tree libgpd.so (the C-ABI in include/gpd.h).
+
+The product path has no CPU fallback: if the HIP library is missing this module
+raises at import, and every decode goes through gpd_decode / gpd_decode_host.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgpd.so")
+
+GPD_ABI_VERSION = 1
+GPD_OK = 0
+
+
+class GpdConfig(C.Structure):
+    _fields_ = [("first_layer", C.c_uint32), ("decoders", C.c_uint32), ("options", C.c_uint32),
+                ("reserved", C.c_uint32), ("ethertype", C.c_void_p), ("ipproto", C.c_void_p),
+                ("tcp_port", C.c_void_p), ("udp_port", C.c_void_p)]
+
+
+class GpdBatch(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("data_len", C.c_uint64), ("offset", C.c_void_p),
+                ("caplen", C.c_void_p), ("n", C.c_uint64)]
+
+
+class GpdResult(C.Structure):
+    _fields_ = [("status", C.c_void_p), ("layers", C.c_void_p), ("net_hash", C.c_void_p),
+                ("tp_hash", C.c_void_p), ("csum", C.c_void_p), ("ext", C.c_void_p)]
+
+
+EXPORTS = {
+    # name: (restype, argtypes)
+    "gpd_abi_version": (C.c_int, []),
+    "gpd_default_tables": (None, [C.c_void_p] * 4),
+    "gpd_ctx_create": (C.c_int, [C.c_int, C.POINTER(GpdConfig), C.POINTER(C.c_void_p)]),
+    "gpd_ctx_reload_tables": (C.c_int, [C.c_void_p, C.POINTER(GpdConfig)]),
+    "gpd_ctx_destroy": (C.c_int, [C.c_void_p]),
+    "gpd_decode": (C.c_int, [C.c_void_p, C.POINTER(GpdBatch), C.POINTER(GpdResult), C.c_void_p]),
+    "gpd_decode_host": (C.c_int, [C.c_void_p, C.POINTER(GpdBatch), C.POINTER(GpdResult)]),
+    "gpd_sync": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "gpd_ctx_set_timing": (C.c_int, [C.c_void_p, C.c_int]),
+    "gpd_last_kernel_ms": (C.c_float, [C.c_void_p]),
+    "gpd_last_error_string": (C.c_char_p, []),
+}
+
+
+class GpdError(RuntimeError):
+    pass
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"gopacket_amd: native library {LIB_PATH} is missing — build it with "
+            "`python -m gopacket_amd.build` (hipcc, gfx950); there is no CPU fallback")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in EXPORTS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.gpd_abi_version() != GPD_ABI_VERSION:
+        raise ImportError("gopacket_amd: libgpd.so ABI version mismatch")
+    return lib
+
+
+lib = _load()
+
+
+def check(rc: int, what: str) -> None:
+    if rc != GPD_OK:
+        msg = lib.gpd_last_error_string()
+        raise GpdError(f"{what}: rc={rc}: {msg.decode() if msg else ''}")

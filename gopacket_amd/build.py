@@ -1,0 +1,59 @@
+"""Build the in-tree native libraries.
+
+  gopacket_amd/libgpd.so       product: HIP kernels (gfx950) + C-ABI runtime (include/gpd.h)
+  oracle/libgpd_oracle.so      test infrastructure: CPU restatement (oracle/)
+
+Both are built with plain compiler invocations (hipcc / gcc); no cmake.  The .so
+files are git-ignored and travel to the GPU box with the repository snapshot.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "gopacket_amd")
+CSRC = os.path.join(PKG, "csrc")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("GPD_OFFLOAD_ARCH", "gfx950")
+
+LIB = os.path.join(PKG, "libgpd.so")
+ORACLE_LIB = os.path.join(ROOT, "oracle", "libgpd_oracle.so")
+
+SOURCES = [os.path.join(CSRC, "gpd_kernels.hip"), os.path.join(CSRC, "gpd_runtime.cpp")]
+HEADERS = [os.path.join(CSRC, "gpd_internal.h"), os.path.join(ROOT, "include", "gpd.h")]
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_lib(force: bool = False, verbose: bool = False) -> str:
+    if force or _stale(LIB, SOURCES + HEADERS):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+               "-Wall", "-Wno-unused-function", "-I", os.path.join(ROOT, "include"),
+               *SOURCES, "-o", LIB + ".tmp"]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+def build_oracle(force: bool = False) -> str:
+    src = [os.path.join(ROOT, "oracle", "gpd_oracle.c"), os.path.join(ROOT, "oracle", "gpd_oracle.h"),
+           os.path.join(ROOT, "include", "gpd.h")]
+    if force or _stale(ORACLE_LIB, src):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "-B" if force else "all"],
+                       check=True)
+    return ORACLE_LIB
+
+
+if __name__ == "__main__":
+    force = "--force" in sys.argv
+    print(build_lib(force=force, verbose=True))
+    print(build_oracle(force=force))

@@ -1,0 +1,406 @@
+// gpd_runtime.cpp — host runtime behind the C-ABI in include/gpd.h.
+//
+// Owns the per-(thread, GPU) context: the snapshot of the dispatch tables in
+// device memory (the reference reads mutable package globals on every packet,
+// layers/enums.go:288-345, layers/ports.go:62-128; a context freezes them at
+// creation like a parser built from them), the registered-decoder mask and
+// options (parser.go:182-195, 336-350), HIP timing events, and the pinned
+// staging used by gpd_decode_host.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <vector>
+
+#include "gpd_internal.h"
+
+namespace {
+
+thread_local char g_err[512] = "";
+
+int set_err(int code, const char *fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof g_err, fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                    \
+  do {                                                                                   \
+    hipError_t e_ = (expr);                                                              \
+    if (e_ != hipSuccess)                                                                \
+      return set_err(GPD_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_));        \
+  } while (0)
+
+// Reference defaults, restated as data: layers/enums.go:304-345, layers/ports.go:62-74,105-122.
+const uint32_t kEtherDefaults[][2] = {
+    {0x0000, 22}, {0x0800, 20}, {0x86DD, 21}, {0x0806, 10}, {0x8100, 15}, {0x880B, 25},
+    {0x8863, 26}, {0x8864, 26}, {0x9000, 12}, {0x2000, 11}, {0x01A2, 61}, {0x88CC, 58},
+    {0x8847, 24}, {0x8848, 24}, {0x888E, 56}, {0x88A8, 15}, {0x6558, 17}, {0x88BE, 145}};
+const uint32_t kProtoDefaults[][2] = {
+    {4, 20},  {6, 44},  {17, 45}, {1, 19},  {58, 57},  {132, 28}, {41, 21}, {94, 20},
+    {97, 16}, {27, 27}, {47, 18}, {0, 46},  {43, 47},  {44, 48},  {60, 49}, {89, 123},
+    {51, 50}, {50, 51}, {136, 52}, {137, 24}, {59, 2}, {2, 62}, {112, 119}};
+const uint32_t kTcpDefaults[][2] = {{53, 107}, {443, 140}, {502, 141}, {636, 140},
+                                    {989, 140}, {990, 140}, {992, 140}, {993, 140},
+                                    {994, 140}, {995, 140}, {5061, 140}};
+const uint32_t kUdpDefaults[][2] = {{53, 107},   {123, 117},  {4789, 116}, {67, 118},
+                                    {68, 118},   {546, 134},  {547, 134},  {666, 147},
+                                    {1000, 149}, {5060, 133}, {6343, 114}, {6081, 120},
+                                    {3784, 122}, {2152, 129}, {623, 142},  {1812, 146}};
+
+template <size_t N>
+void fill(uint16_t *t, size_t size, const uint32_t (&e)[N][2]) {
+  memset(t, 0, size * sizeof(uint16_t));
+  for (size_t k = 0; k < N; k++) t[e[k][0]] = (uint16_t)e[k][1];
+}
+
+// Two-level page encoding of the three 64K tables (see gpd_internal.h).
+std::vector<uint16_t> encode_tables(const uint16_t *eth, const uint16_t *proto,
+                                    const uint16_t *tcp, const uint16_t *udp) {
+  std::vector<uint16_t> out(gpd::kTabPages + 256, 0);  // page 0 = zeros
+  std::memcpy(out.data() + gpd::kTabIpProto, proto, 256 * sizeof(uint16_t));
+  std::map<std::vector<uint16_t>, uint16_t> pages;
+  pages[std::vector<uint16_t>(256, 0)] = 0;
+  auto encode = [&](const uint16_t *t, uint32_t dir) {
+    for (uint32_t hi = 0; hi < 256; hi++) {
+      std::vector<uint16_t> pg(t + hi * 256, t + hi * 256 + 256);
+      auto it = pages.find(pg);
+      uint16_t idx;
+      if (it == pages.end()) {
+        idx = (uint16_t)pages.size();
+        pages[pg] = idx;
+        out.insert(out.end(), pg.begin(), pg.end());
+      } else {
+        idx = it->second;
+      }
+      out[dir + hi] = idx;
+    }
+  };
+  encode(eth, gpd::kTabEthDir);
+  encode(tcp, gpd::kTabTcpDir);
+  encode(udp, gpd::kTabUdpDir);
+  return out;
+}
+
+}  // namespace
+
+struct gpd_ctx {
+  int device = 0;
+  int num_cus = 256;
+  uint32_t first = GPD_LT_ETHERNET;
+  uint32_t decoders = GPD_DEC_ALL;
+  uint32_t options = 0;
+  uint16_t *d_tables = nullptr;
+  size_t tables_words = 0;
+  bool timing = false;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool timed = false;
+  // gpd_decode_host staging (two slots)
+  struct Slot {
+    hipStream_t stream = nullptr;
+    uint8_t *h_data = nullptr, *d_data = nullptr;
+    uint32_t *h_off = nullptr, *h_len = nullptr, *d_off = nullptr, *d_len = nullptr;
+    uint32_t *h_status = nullptr, *d_status = nullptr, *h_csum = nullptr, *d_csum = nullptr;
+    uint64_t *h_layers = nullptr, *d_layers = nullptr, *h_nh = nullptr, *d_nh = nullptr;
+    uint64_t *h_th = nullptr, *d_th = nullptr;
+    gpd_ext_rec *h_ext = nullptr, *d_ext = nullptr;
+    uint64_t lo = 0, hi = 0;  // packet range in flight
+    bool busy = false;
+  } slot[2];
+  uint64_t slot_bytes = 0, slot_pkts = 0;
+};
+
+extern "C" {
+
+int gpd_abi_version(void) { return GPD_ABI_VERSION; }
+
+const char *gpd_last_error_string(void) { return g_err; }
+
+void gpd_default_tables(uint16_t *ethertype, uint16_t *ipproto, uint16_t *tcp_port,
+                        uint16_t *udp_port) {
+  if (ethertype) fill(ethertype, 65536, kEtherDefaults);
+  if (ipproto) fill(ipproto, 256, kProtoDefaults);
+  if (tcp_port) fill(tcp_port, 65536, kTcpDefaults);
+  if (udp_port) fill(udp_port, 65536, kUdpDefaults);
+}
+
+int gpd_ctx_reload_tables(gpd_ctx *ctx, const gpd_config *cfg) {
+  if (!ctx || !cfg) return set_err(GPD_ERR_INVALID, "gpd_ctx_reload_tables: null argument");
+  std::vector<uint16_t> eth(65536), proto(256), tcp(65536), udp(65536);
+  gpd_default_tables(eth.data(), proto.data(), tcp.data(), udp.data());
+  if (cfg->ethertype) std::memcpy(eth.data(), cfg->ethertype, 65536 * 2);
+  if (cfg->ipproto) std::memcpy(proto.data(), cfg->ipproto, 256 * 2);
+  if (cfg->tcp_port) std::memcpy(tcp.data(), cfg->tcp_port, 65536 * 2);
+  if (cfg->udp_port) std::memcpy(udp.data(), cfg->udp_port, 65536 * 2);
+  std::vector<uint16_t> blob = encode_tables(eth.data(), proto.data(), tcp.data(), udp.data());
+  HIP_TRY(hipSetDevice(ctx->device));
+  if (ctx->d_tables && ctx->tables_words < blob.size()) {
+    HIP_TRY(hipFree(ctx->d_tables));
+    ctx->d_tables = nullptr;
+  }
+  if (!ctx->d_tables) {
+    HIP_TRY(hipMalloc(&ctx->d_tables, blob.size() * sizeof(uint16_t)));
+    ctx->tables_words = blob.size();
+  }
+  HIP_TRY(hipMemcpy(ctx->d_tables, blob.data(), blob.size() * sizeof(uint16_t),
+                    hipMemcpyHostToDevice));
+  return GPD_OK;
+}
+
+int gpd_ctx_create(int device, const gpd_config *cfg, gpd_ctx **out) {
+  if (!out) return set_err(GPD_ERR_INVALID, "gpd_ctx_create: out is NULL");
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+    return set_err(GPD_ERR_NODEVICE, "gpd_ctx_create: no HIP device available");
+  if (device < 0 || device >= ndev)
+    return set_err(GPD_ERR_INVALID, "gpd_ctx_create: device %d out of range [0,%d)", device, ndev);
+  gpd_config defaults{};
+  defaults.first_layer = GPD_LT_ETHERNET;
+  defaults.decoders = GPD_DEC_ALL;
+  if (!cfg) cfg = &defaults;
+  if (cfg->decoders & ~GPD_DEC_ALL)
+    return set_err(GPD_ERR_INVALID, "gpd_ctx_create: unknown decoder bits 0x%x", cfg->decoders);
+  gpd_ctx *ctx = new gpd_ctx;
+  ctx->device = device;
+  ctx->first = cfg->first_layer;
+  ctx->decoders = cfg->decoders;
+  ctx->options = cfg->options;
+  hipDeviceProp_t prop;
+  if (hipSetDevice(device) != hipSuccess || hipGetDeviceProperties(&prop, device) != hipSuccess) {
+    delete ctx;
+    return set_err(GPD_ERR_HIP, "gpd_ctx_create: cannot query device %d", device);
+  }
+  ctx->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+  int rc = gpd_ctx_reload_tables(ctx, cfg);
+  if (rc) {
+    delete ctx;
+    return rc;
+  }
+  *out = ctx;
+  return GPD_OK;
+}
+
+static void free_slots(gpd_ctx *ctx) {
+  for (auto &s : ctx->slot) {
+    if (s.stream) (void)hipStreamSynchronize(s.stream);
+    for (void *p : {(void *)s.h_data, (void *)s.h_off, (void *)s.h_len, (void *)s.h_status,
+                    (void *)s.h_csum, (void *)s.h_layers, (void *)s.h_nh, (void *)s.h_th,
+                    (void *)s.h_ext})
+      if (p) (void)hipHostFree(p);
+    for (void *p : {(void *)s.d_data, (void *)s.d_off, (void *)s.d_len, (void *)s.d_status,
+                    (void *)s.d_csum, (void *)s.d_layers, (void *)s.d_nh, (void *)s.d_th,
+                    (void *)s.d_ext})
+      if (p) (void)hipFree(p);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+    s = gpd_ctx::Slot{};
+  }
+  ctx->slot_bytes = ctx->slot_pkts = 0;
+}
+
+int gpd_ctx_destroy(gpd_ctx *ctx) {
+  if (!ctx) return GPD_OK;
+  (void)hipSetDevice(ctx->device);
+  free_slots(ctx);
+  if (ctx->d_tables) (void)hipFree(ctx->d_tables);
+  if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+  if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+  delete ctx;
+  return GPD_OK;
+}
+
+int gpd_ctx_set_timing(gpd_ctx *ctx, int enable) {
+  if (!ctx) return set_err(GPD_ERR_INVALID, "gpd_ctx_set_timing: null ctx");
+  HIP_TRY(hipSetDevice(ctx->device));
+  if (enable && !ctx->ev0) {
+    HIP_TRY(hipEventCreate(&ctx->ev0));
+    HIP_TRY(hipEventCreate(&ctx->ev1));
+  }
+  ctx->timing = enable != 0;
+  ctx->timed = false;
+  return GPD_OK;
+}
+
+float gpd_last_kernel_ms(gpd_ctx *ctx) {
+  if (!ctx || !ctx->timed) return -1.0f;
+  float ms = -1.0f;
+  if (hipEventSynchronize(ctx->ev1) != hipSuccess) return -1.0f;
+  if (hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1) != hipSuccess) return -1.0f;
+  return ms;
+}
+
+static int check_batch(const gpd_batch *in, const gpd_result *out) {
+  if (!in || !out) return set_err(GPD_ERR_INVALID, "gpd_decode: null batch or result");
+  if (in->n == 0) return GPD_OK;
+  if (!in->data || !in->offset || !in->caplen)
+    return set_err(GPD_ERR_INVALID, "gpd_decode: batch data/offset/caplen must be non-NULL");
+  if (!out->status || !out->layers)
+    return set_err(GPD_ERR_INVALID, "gpd_decode: result status/layers must be non-NULL");
+  if ((reinterpret_cast<uintptr_t>(in->data) & 15) != 0)
+    return set_err(GPD_ERR_INVALID, "gpd_decode: data pointer must be 16-byte aligned");
+  if (in->data_len > 0xFFFFFFF0ull)
+    return set_err(GPD_ERR_INVALID, "gpd_decode: data_len %llu exceeds the 32-bit offset range",
+                   (unsigned long long)in->data_len);
+  return GPD_OK;
+}
+
+static int launch(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, hipStream_t stream,
+                  bool record) {
+  gpd::KParams P{};
+  P.data = in->data;
+  P.data_len = in->data_len;
+  P.offset = in->offset;
+  P.caplen = in->caplen;
+  P.n = in->n;
+  P.status = out->status;
+  P.layers = out->layers;
+  P.net_hash = out->net_hash;
+  P.tp_hash = out->tp_hash;
+  P.csum = out->csum;
+  P.ext = out->ext;
+  P.tables = ctx->d_tables;
+  P.first = ctx->first;
+  P.decoders = ctx->decoders;
+  P.options = ctx->options;
+  if (record) HIP_TRY(hipEventRecord(ctx->ev0, stream));
+  hipError_t e = gpd::launch_decode(P, stream, ctx->num_cus);
+  if (e != hipSuccess) return set_err(GPD_ERR_HIP, "decode kernel launch: %s", hipGetErrorString(e));
+  if (record) {
+    HIP_TRY(hipEventRecord(ctx->ev1, stream));
+    ctx->timed = true;
+  }
+  return GPD_OK;
+}
+
+int gpd_decode(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, void *stream) {
+  if (!ctx) return set_err(GPD_ERR_INVALID, "gpd_decode: null ctx");
+  int rc = check_batch(in, out);
+  if (rc || in->n == 0) return rc;
+  HIP_TRY(hipSetDevice(ctx->device));
+  return launch(ctx, in, out, (hipStream_t)stream, ctx->timing);
+}
+
+int gpd_sync(gpd_ctx *ctx, void *stream) {
+  if (!ctx) return set_err(GPD_ERR_INVALID, "gpd_sync: null ctx");
+  HIP_TRY(hipSetDevice(ctx->device));
+  HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  return GPD_OK;
+}
+
+// ---- host-memory path: chunked, double-buffered pinned H2D -> decode -> D2H ----
+static int alloc_slots(gpd_ctx *ctx, uint64_t bytes, uint64_t pkts, bool ext) {
+  if (ctx->slot_bytes >= bytes && ctx->slot_pkts >= pkts && (!ext || ctx->slot[0].d_ext))
+    return GPD_OK;
+  free_slots(ctx);
+  for (auto &s : ctx->slot) {
+    HIP_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+    HIP_TRY(hipHostMalloc(&s.h_data, bytes + 64, hipHostMallocDefault));
+    HIP_TRY(hipMalloc(&s.d_data, bytes + 64));
+    HIP_TRY(hipHostMalloc(&s.h_off, pkts * 4, hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc(&s.h_len, pkts * 4, hipHostMallocDefault));
+    HIP_TRY(hipMalloc(&s.d_off, pkts * 4));
+    HIP_TRY(hipMalloc(&s.d_len, pkts * 4));
+    HIP_TRY(hipHostMalloc(&s.h_status, pkts * 4, hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc(&s.h_csum, pkts * 4, hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc(&s.h_layers, pkts * 8, hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc(&s.h_nh, pkts * 8, hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc(&s.h_th, pkts * 8, hipHostMallocDefault));
+    HIP_TRY(hipMalloc(&s.d_status, pkts * 4));
+    HIP_TRY(hipMalloc(&s.d_csum, pkts * 4));
+    HIP_TRY(hipMalloc(&s.d_layers, pkts * 8));
+    HIP_TRY(hipMalloc(&s.d_nh, pkts * 8));
+    HIP_TRY(hipMalloc(&s.d_th, pkts * 8));
+    if (ext) {
+      HIP_TRY(hipHostMalloc(&s.h_ext, pkts * sizeof(gpd_ext_rec), hipHostMallocDefault));
+      HIP_TRY(hipMalloc(&s.d_ext, pkts * sizeof(gpd_ext_rec)));
+    }
+  }
+  ctx->slot_bytes = bytes;
+  ctx->slot_pkts = pkts;
+  return GPD_OK;
+}
+
+static void drain_slot(gpd_ctx::Slot &s, const gpd_result *out) {
+  const uint64_t m = s.hi - s.lo;
+  std::memcpy(out->status + s.lo, s.h_status, m * 4);
+  std::memcpy(out->layers + s.lo, s.h_layers, m * 8);
+  if (out->csum) std::memcpy(out->csum + s.lo, s.h_csum, m * 4);
+  if (out->net_hash) std::memcpy(out->net_hash + s.lo, s.h_nh, m * 8);
+  if (out->tp_hash) std::memcpy(out->tp_hash + s.lo, s.h_th, m * 8);
+  if (out->ext) std::memcpy(out->ext + s.lo, s.h_ext, m * sizeof(gpd_ext_rec));
+  s.busy = false;
+}
+
+int gpd_decode_host(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out) {
+  if (!ctx) return set_err(GPD_ERR_INVALID, "gpd_decode_host: null ctx");
+  if (!in || !out || !out->status || !out->layers)
+    return set_err(GPD_ERR_INVALID, "gpd_decode_host: null batch/result");
+  if (in->n == 0) return GPD_OK;
+  HIP_TRY(hipSetDevice(ctx->device));
+  const uint64_t kPkts = 1u << 20, kBytes = 256ull << 20;
+  int rc = alloc_slots(ctx, kBytes, kPkts, out->ext != nullptr);
+  if (rc) return rc;
+  uint64_t i = 0;
+  int k = 0;
+  while (i < in->n) {
+    auto &s = ctx->slot[k];
+    if (s.busy) {
+      HIP_TRY(hipStreamSynchronize(s.stream));
+      drain_slot(s, out);
+    }
+    // gather packets [i, j) whose bytes fit the slot, rebased to a 16-aligned start
+    uint64_t j = i, used = 0;
+    while (j < in->n && j - i < kPkts) {
+      const uint32_t len = in->caplen[j];
+      const uint64_t need = ((used + 15) & ~15ull) + len;
+      if (need > kBytes) break;
+      used = need;
+      j++;
+    }
+    if (j == i) return set_err(GPD_ERR_INVALID, "gpd_decode_host: packet %llu larger than %llu bytes",
+                               (unsigned long long)i, (unsigned long long)kBytes);
+    uint64_t pos = 0;
+    for (uint64_t p = i; p < j; p++) {
+      pos = (pos + 15) & ~15ull;
+      const uint32_t len = in->caplen[p];
+      std::memcpy(s.h_data + pos, in->data + in->offset[p], len);
+      s.h_off[p - i] = (uint32_t)pos;
+      s.h_len[p - i] = len;
+      pos += len;
+    }
+    const uint64_t m = j - i;
+    HIP_TRY(hipMemcpyAsync(s.d_data, s.h_data, (pos + 15) & ~15ull, hipMemcpyHostToDevice, s.stream));
+    HIP_TRY(hipMemcpyAsync(s.d_off, s.h_off, m * 4, hipMemcpyHostToDevice, s.stream));
+    HIP_TRY(hipMemcpyAsync(s.d_len, s.h_len, m * 4, hipMemcpyHostToDevice, s.stream));
+    gpd_batch b{s.d_data, pos, s.d_off, s.d_len, m};
+    gpd_result r{s.d_status, s.d_layers, s.d_nh, s.d_th, s.d_csum, out->ext ? s.d_ext : nullptr};
+    rc = launch(ctx, &b, &r, s.stream, false);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(s.h_status, s.d_status, m * 4, hipMemcpyDeviceToHost, s.stream));
+    HIP_TRY(hipMemcpyAsync(s.h_layers, s.d_layers, m * 8, hipMemcpyDeviceToHost, s.stream));
+    if (out->csum) HIP_TRY(hipMemcpyAsync(s.h_csum, s.d_csum, m * 4, hipMemcpyDeviceToHost, s.stream));
+    if (out->net_hash) HIP_TRY(hipMemcpyAsync(s.h_nh, s.d_nh, m * 8, hipMemcpyDeviceToHost, s.stream));
+    if (out->tp_hash) HIP_TRY(hipMemcpyAsync(s.h_th, s.d_th, m * 8, hipMemcpyDeviceToHost, s.stream));
+    if (out->ext)
+      HIP_TRY(hipMemcpyAsync(s.h_ext, s.d_ext, m * sizeof(gpd_ext_rec), hipMemcpyDeviceToHost, s.stream));
+    s.lo = i;
+    s.hi = j;
+    s.busy = true;
+    i = j;
+    k ^= 1;
+  }
+  for (auto &s : ctx->slot) {
+    if (s.busy) {
+      HIP_TRY(hipStreamSynchronize(s.stream));
+      drain_slot(s, out);
+    }
+  }
+  return GPD_OK;
+}
+
+}  // extern "C"

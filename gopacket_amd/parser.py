@@ -1,0 +1,267 @@
+"""DecodingLayerParser — the reference's parser surface over the MI355X engine.
+
+Mirrors gopacket's API (parser.go:182-350) with batch entry points added:
+
+    eth, ip4, tcp, payload = Ethernet(), IPv4(), TCP(), Payload()
+    parser = NewDecodingLayerParser(LayerTypeEthernet, eth, ip4, tcp, payload)
+    parser.IgnoreUnsupported = True
+    res = parser.DecodeBatch(batch)          # one kernel launch for the whole batch
+    res.decoded(i), res.err(i), res.truncated(i), res.network_flow_hash(i) ...
+    err = parser.DecodeLayers(data, decoded) # single packet, same call shape as Go
+
+The decoder objects only select which DecodingLayers are registered (their
+CanDecode sets); decoding runs in the HIP kernel through the C-ABI
+(include/gpd.h).  A parser snapshots the dispatch tables (layers.TABLES) when
+its device context is created; call reload_tables() after Register*().
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import numpy as np
+
+from . import layers as L
+from ._lib import GpdBatch, GpdConfig, GpdResult, check, lib
+from .batch import PacketBatch
+from .results import EXT_DTYPE, BatchResult
+
+DEC_ETHERNET, DEC_DOT1Q, DEC_IPV4, DEC_IPV6, DEC_IPV6_EXT = 1, 2, 4, 8, 16
+DEC_TCP, DEC_UDP, DEC_VXLAN, DEC_PAYLOAD, DEC_FRAGMENT = 32, 64, 128, 256, 512
+OPT_IGNORE_UNSUPPORTED, OPT_IGNORE_PANIC = 1, 2
+OPT_NO_CHECKSUMS, OPT_NO_FLOW_HASH = 256, 512
+
+
+class DecodingLayer:
+    """A registrable decoder (parser.go:29-46); `bit` selects it in the kernel."""
+    bit = 0
+    can_decode: tuple = ()
+
+    def CanDecode(self):
+        return self.can_decode
+
+
+class Ethernet(DecodingLayer):      # layers/ethernet.go:106-108
+    bit, can_decode = DEC_ETHERNET, (L.LayerTypeEthernet,)
+
+
+class Dot1Q(DecodingLayer):         # layers/dot1q.go:43-45
+    bit, can_decode = DEC_DOT1Q, (L.LayerTypeDot1Q,)
+
+
+class IPv4(DecodingLayer):          # layers/ip4.go:277-279
+    bit, can_decode = DEC_IPV4, (L.LayerTypeIPv4,)
+
+
+class IPv6(DecodingLayer):          # layers/ip6.go:281-283
+    bit, can_decode = DEC_IPV6, (L.LayerTypeIPv6,)
+
+
+class IPv6ExtensionSkipper(DecodingLayer):  # layers/ip6.go:454-456
+    bit, can_decode = DEC_IPV6_EXT, L.LayerClassIPv6Extension
+
+
+class TCP(DecodingLayer):           # layers/tcp.go:304-306
+    bit, can_decode = DEC_TCP, (L.LayerTypeTCP,)
+
+
+class UDP(DecodingLayer):           # layers/udp.go:98-100
+    bit, can_decode = DEC_UDP, (L.LayerTypeUDP,)
+
+
+class VXLAN(DecodingLayer):         # layers/vxlan.go:43-45
+    bit, can_decode = DEC_VXLAN, (L.LayerTypeVXLAN,)
+
+
+class Payload(DecodingLayer):       # base.go:54
+    bit, can_decode = DEC_PAYLOAD, (L.LayerTypePayload,)
+
+
+class Fragment(DecodingLayer):      # base.go:111
+    bit, can_decode = DEC_FRAGMENT, (L.LayerTypeFragment,)
+
+
+DECODER_BY_NAME = {c.__name__: c for c in (Ethernet, Dot1Q, IPv4, IPv6, IPv6ExtensionSkipper, TCP,
+                                            UDP, VXLAN, Payload, Fragment)}
+
+
+def decoder_mask(decoders) -> int:
+    m = 0
+    for d in decoders:
+        if isinstance(d, str):
+            d = DECODER_BY_NAME[d]
+        if isinstance(d, type):
+            d = d()
+        if not isinstance(d, DecodingLayer):
+            raise TypeError(f"{d!r} is not a DecodingLayer this engine implements")
+        m |= d.bit
+    return m
+
+
+def _torch():
+    import torch
+    if not torch.cuda.is_available():
+        raise RuntimeError("gopacket_amd: no GPU visible to torch; the decode path runs only on HIP")
+    return torch
+
+
+class _Ctx:
+    def __init__(self, device: int, first: int, mask: int, options: int, tables: L.DispatchTables):
+        self.tables = tables.copy()
+        cfg = self._cfg(first, mask, options)
+        h = C.c_void_p()
+        check(lib.gpd_ctx_create(device, C.byref(cfg), C.byref(h)), "gpd_ctx_create")
+        self.h = h
+        self.key = (device, first, mask, options)
+
+    def _cfg(self, first, mask, options):
+        t = self.tables
+        return GpdConfig(first, mask, options, 0, t.ethertype.ctypes.data, t.ipproto.ctypes.data,
+                         t.tcp_port.ctypes.data, t.udp_port.ctypes.data)
+
+    def reload(self, tables: L.DispatchTables):
+        self.tables = tables.copy()
+        cfg = self._cfg(*self.key[1:])
+        check(lib.gpd_ctx_reload_tables(self.h, C.byref(cfg)), "gpd_ctx_reload_tables")
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and h.value:
+            lib.gpd_ctx_destroy(h)
+            self.h = None
+
+
+class DeviceBatch:
+    """A PacketBatch resident in HBM (torch tensors on `device`)."""
+
+    def __init__(self, batch: PacketBatch, device: int = 0):
+        torch = _torch()
+        dev = torch.device("cuda", device)
+        self.n = batch.n
+        self.data_len = batch.data_len
+        self.data = torch.from_numpy(batch.data).to(dev)
+        self.offset = torch.from_numpy(batch.offset.view(np.int32)).to(dev)
+        self.caplen = torch.from_numpy(batch.caplen.view(np.int32)).to(dev)
+        self.device = device
+
+    def c_batch(self) -> GpdBatch:
+        return GpdBatch(self.data.data_ptr(), self.data_len, self.offset.data_ptr(),
+                        self.caplen.data_ptr(), self.n)
+
+
+class DeviceResult:
+    """Result SoA in HBM; .to_host() gives a BatchResult."""
+
+    def __init__(self, n: int, device: int = 0, ext: bool = False):
+        torch = _torch()
+        dev = torch.device("cuda", device)
+        self.n = n
+        self.status = torch.empty(n, dtype=torch.int32, device=dev)
+        self.layers = torch.empty(n, dtype=torch.int64, device=dev)
+        self.net_hash = torch.empty(n, dtype=torch.int64, device=dev)
+        self.tp_hash = torch.empty(n, dtype=torch.int64, device=dev)
+        self.csum = torch.empty(n, dtype=torch.int32, device=dev)
+        self.ext = torch.empty(n * EXT_DTYPE.itemsize, dtype=torch.uint8, device=dev) if ext else None
+
+    def c_result(self) -> GpdResult:
+        return GpdResult(self.status.data_ptr(), self.layers.data_ptr(), self.net_hash.data_ptr(),
+                         self.tp_hash.data_ptr(), self.csum.data_ptr(),
+                         self.ext.data_ptr() if self.ext is not None else None)
+
+    def to_host(self) -> BatchResult:
+        u = lambda t, dt: t.cpu().numpy().view(dt)
+        return BatchResult(u(self.status, np.uint32), u(self.layers, np.uint64),
+                           u(self.net_hash, np.uint64), u(self.tp_hash, np.uint64),
+                           u(self.csum, np.uint32),
+                           self.ext.cpu().numpy().view(EXT_DTYPE) if self.ext is not None else None)
+
+
+class DecodingLayerParser:
+    """parser.go:182-195 (DecodingLayerParser) + :336-350 (options)."""
+
+    def __init__(self, first: int, *decoders, device: int = 0):
+        self.first = int(first)
+        self._mask = decoder_mask(decoders)
+        self.IgnoreUnsupported = False
+        self.IgnorePanic = False
+        self.ComputeChecksums = True   # engine knob: the fused ComputeChecksum / ip4 checksum
+        self.ComputeFlowHashes = True  # engine knob: the fused FastHash
+        self.Truncated = False
+        self.device = device
+        self._ctx: Optional[_Ctx] = None
+        self._tables = L.TABLES.copy()
+
+    # --- registration (parser.go:197-241) ---------------------------------------
+    def AddDecodingLayer(self, d) -> None:
+        self._mask |= decoder_mask([d])
+
+    @property
+    def decoders(self) -> int:
+        return self._mask
+
+    def reload_tables(self) -> None:
+        """Re-snapshot layers.TABLES (after RegisterTCPPortLayerType etc.)."""
+        self._tables = L.TABLES.copy()
+        if self._ctx is not None:
+            self._ctx.reload(self._tables)
+
+    @property
+    def options(self) -> int:
+        o = OPT_IGNORE_UNSUPPORTED if self.IgnoreUnsupported else 0
+        o |= OPT_IGNORE_PANIC if self.IgnorePanic else 0
+        o |= 0 if self.ComputeChecksums else OPT_NO_CHECKSUMS
+        o |= 0 if self.ComputeFlowHashes else OPT_NO_FLOW_HASH
+        return o
+
+    def ctx(self) -> _Ctx:
+        key = (self.device, self.first, self._mask, self.options)
+        if self._ctx is None or self._ctx.key != key:
+            self._ctx = _Ctx(self.device, self.first, self._mask, self.options, self._tables)
+        return self._ctx
+
+    # --- decoding -----------------------------------------------------------------
+    def decode_device(self, dbatch: DeviceBatch, dres: DeviceResult, stream=None) -> None:
+        """Asynchronous decode of an HBM-resident batch on `stream` (torch stream or None =
+        torch's current stream)."""
+        torch = _torch()
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device)
+        b, r = dbatch.c_batch(), dres.c_result()
+        check(lib.gpd_decode(self.ctx().h, C.byref(b), C.byref(r), C.c_void_p(stream.cuda_stream)),
+              "gpd_decode")
+
+    def DecodeBatch(self, batch: PacketBatch, ext: bool = False) -> BatchResult:
+        """Decode every packet of a host batch on the GPU (H2D, kernel, D2H)."""
+        torch = _torch()
+        db = DeviceBatch(batch, self.device)
+        dr = DeviceResult(batch.n, self.device, ext)
+        self.decode_device(db, dr)
+        torch.cuda.synchronize(self.device)
+        return dr.to_host()
+
+    def DecodeBatchHost(self, batch: PacketBatch, ext: bool = False) -> BatchResult:
+        """Host-memory path through gpd_decode_host (pinned, chunked, double-buffered)."""
+        n = batch.n
+        res = BatchResult(np.zeros(n, np.uint32), np.zeros(n, np.uint64), np.zeros(n, np.uint64),
+                          np.zeros(n, np.uint64), np.zeros(n, np.uint32),
+                          np.zeros(n, EXT_DTYPE) if ext else None)
+        b = GpdBatch(batch.data.ctypes.data, batch.data_len, batch.offset.ctypes.data,
+                     batch.caplen.ctypes.data, n)
+        r = GpdResult(res.status.ctypes.data, res.layers.ctypes.data, res.net_hash.ctypes.data,
+                      res.tp_hash.ctypes.data, res.csum.ctypes.data,
+                      res.ext.ctypes.data if ext else None)
+        check(lib.gpd_decode_host(self.ctx().h, C.byref(b), C.byref(r)), "gpd_decode_host")
+        return res
+
+    def DecodeLayers(self, data: bytes, decoded: list):
+        """parser.go:302-316 for one packet: fills `decoded`, sets self.Truncated, returns the
+        error value (None on success)."""
+        res = self.DecodeBatch(PacketBatch.from_packets([data]), ext=True)
+        decoded[:] = res.decoded(0)
+        self.Truncated = res.truncated(0)
+        return res.err(0)
+
+
+def NewDecodingLayerParser(first: int, *decoders, device: int = 0) -> DecodingLayerParser:
+    """parser.go:222-233."""
+    return DecodingLayerParser(first, *decoders, device=device)

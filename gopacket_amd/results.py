@@ -1,0 +1,125 @@
+"""Per-packet result words (include/gpd.h) and their reading as gopacket values.
+
+BatchResult answers, per packet index, what the reference's caller reads after
+`err := parser.DecodeLayers(data, &decoded)` (parser.go:302-316): the decoded
+slice, the error value (exact text), parser.Truncated, the flows' FastHash
+(flows.go:167-174), the IPv4 header checksum (ip4.go:158-179) and
+TCP.ComputeChecksum() (tcp.go:193-195).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+from .errors import DecodeError, UnsupportedLayerType
+from .layers import CODE_TO_LAYERTYPE
+
+OBJ_NAMES = ("Ethernet", "Dot1Q", "IPv4", "IPv6", "IPv6ExtensionSkipper", "TCP", "UDP", "VXLAN",
+             "Payload", "Fragment")
+
+LAYER_REC_DTYPE = np.dtype([("contents_off", "<u4"), ("contents_len", "<u4"),
+                            ("payload_off", "<u4"), ("payload_len", "<u4")])
+EXT_DTYPE = np.dtype([("layer_codes", "<u8", (2,)), ("err_arg0", "<u4"), ("err_arg1", "<u4"),
+                      ("obj_valid", "<u2"), ("pad0", "<u2"), ("pad1", "<u4"),
+                      ("obj", LAYER_REC_DTYPE, (10,))])
+assert EXT_DTYPE.itemsize == 192
+
+ST_OK, ST_UNSUPPORTED, ST_DECODE_ERROR = 0, 1, 2
+
+
+def st_class(s):
+    return s & 3
+
+
+def st_truncated(s):
+    return (s >> 2) & 1
+
+
+def st_nlayers(s):
+    return (s >> 4) & 31
+
+
+def st_errcode(s):
+    return (s >> 9) & 63
+
+
+@dataclass
+class BatchResult:
+    status: np.ndarray            # uint32[n]
+    layers: np.ndarray            # uint64[n]
+    net_hash: Optional[np.ndarray] = None
+    tp_hash: Optional[np.ndarray] = None
+    csum: Optional[np.ndarray] = None
+    ext: Optional[np.ndarray] = None  # EXT_DTYPE[n]
+
+    def __len__(self):
+        return int(self.status.shape[0])
+
+    # --- the DecodeLayers outputs -------------------------------------------------
+    def decoded(self, i: int) -> list:
+        """The `decoded` slice (LayerType values), layers_decoder.go:69."""
+        s = int(self.status[i])
+        n = st_nlayers(s)
+        if self.ext is not None:
+            words = self.ext["layer_codes"][i]
+            n = min(n, 32)
+            return [CODE_TO_LAYERTYPE[(int(words[k // 16]) >> (4 * (k % 16))) & 15] for k in range(n)]
+        w = int(self.layers[i])
+        if n > 12:
+            raise ValueError(f"packet {i}: {n} layers exceed the core record; decode with ext=True")
+        return [CODE_TO_LAYERTYPE[(w >> (16 + 4 * k)) & 15] for k in range(n)]
+
+    def stop_type(self, i: int) -> int:
+        """LayerType the loop stopped at for want of a decoder (0 = none)."""
+        return int(self.layers[i]) & 0xFFFF
+
+    def err(self, i: int):
+        """The error DecodeLayers returned: None, UnsupportedLayerType or DecodeError."""
+        s = int(self.status[i])
+        c = st_class(s)
+        if c == ST_OK:
+            return None
+        if c == ST_UNSUPPORTED:
+            return UnsupportedLayerType(self.stop_type(i))
+        a0 = a1 = 0
+        if self.ext is not None:
+            a0, a1 = int(self.ext["err_arg0"][i]), int(self.ext["err_arg1"][i])
+        return DecodeError(st_errcode(s), a0, a1)
+
+    def truncated(self, i: int) -> bool:
+        return bool(st_truncated(int(self.status[i])))
+
+    def network_flow_hash(self, i: int) -> Optional[int]:
+        s = int(self.status[i])
+        return int(self.net_hash[i]) if (s >> 16) & 1 else None
+
+    def transport_flow_hash(self, i: int) -> Optional[int]:
+        s = int(self.status[i])
+        return int(self.tp_hash[i]) if (s >> 17) & 1 else None
+
+    def ip4_checksum(self, i: int) -> Optional[int]:
+        s = int(self.status[i])
+        return int(self.csum[i]) & 0xFFFF if (s >> 18) & 1 else None
+
+    def l4_checksum(self, i: int) -> Optional[int]:
+        s = int(self.status[i])
+        return int(self.csum[i]) >> 16 if (s >> 19) & 1 else None
+
+    def layer(self, i: int, name: str):
+        """(contents, payload) byte ranges of a layer object after the call, or None."""
+        if self.ext is None:
+            raise ValueError("layer records need ext=True")
+        k = OBJ_NAMES.index(name)
+        if not (int(self.ext["obj_valid"][i]) >> k) & 1:
+            return None
+        r = self.ext["obj"][i][k]
+        c0, p0 = int(r["contents_off"]), int(r["payload_off"])
+        return (c0, c0 + int(r["contents_len"])), (p0, p0 + int(r["payload_len"]))
+
+
+def empty_result(n: int, ext: bool = False) -> BatchResult:
+    return BatchResult(np.zeros(n, np.uint32), np.zeros(n, np.uint64), np.zeros(n, np.uint64),
+                       np.zeros(n, np.uint64), np.zeros(n, np.uint32),
+                       np.zeros(n, EXT_DTYPE) if ext else None)

@@ -1,0 +1,266 @@
+"""Deterministic synthetic packet batches for the BASELINE.json configurations.
+
+  config 2  make_udp64(n)   64 B Eth/IPv4/UDP, seed 0x5EED0002
+  config 3  make_imix(n)    IMIX 64/576/1500 (7:4:1) Eth/Dot1Q/IPv4/TCP, seed 0x5EED0003
+  config 4  make_vxlan(n)   128 B Eth/IPv4/UDP:4789/VXLAN/Eth/IPv4/TCP, seed 0x5EED0004
+
+Random fields come from a vectorised splitmix64 stream; ports avoid every key of
+the reference's port tables (layers/ports.go:62-122) so the transport's next layer
+is Payload.  Checksums are valid except for 1 packet in 64, whose checksum is
+corrupted on purpose (IPv4 header for config 2, TCP for configs 3 and 4).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .batch import PAD, PacketBatch
+from .layers import TABLES
+
+_M1 = np.uint64(0xBF58476D1CE4E5B9)
+_M2 = np.uint64(0x94D049BB133111EB)
+_GOLD = np.uint64(0x9E3779B97F4A7C15)
+
+
+def splitmix64(seed: int, n: int, stream: int = 0, base: int = 0) -> np.ndarray:
+    """Outputs base+1 .. base+n of splitmix64 stream `stream` (state seed + stream*2^40)."""
+    with np.errstate(over="ignore"):
+        idx = np.arange(base + 1, base + n + 1, dtype=np.uint64) + \
+            np.uint64((stream << 40) & 0xFFFFFFFFFFFFFFFF)
+        z = np.uint64(seed & 0xFFFFFFFFFFFFFFFF) + idx * _GOLD
+        z = (z ^ (z >> np.uint64(30))) * _M1
+        z = (z ^ (z >> np.uint64(27))) * _M2
+        return z ^ (z >> np.uint64(31))
+
+
+def _free_ports(table: np.ndarray) -> np.ndarray:
+    p = np.arange(1024, 65536, dtype=np.int64)
+    return p[table[p] == 0]
+
+
+def _pick(values: np.ndarray, r: np.ndarray) -> np.ndarray:
+    return values[(r % np.uint64(len(values))).astype(np.int64)]
+
+
+def _be16(a: np.ndarray, col: int, v: np.ndarray) -> None:
+    a[:, col] = (v >> 8) & 0xFF
+    a[:, col + 1] = v & 0xFF
+
+
+def _be32(a: np.ndarray, col: int, v: np.ndarray) -> None:
+    v = v.astype(np.uint64)
+    for k in range(4):
+        a[:, col + k] = ((v >> np.uint64(24 - 8 * k)) & np.uint64(0xFF)).astype(np.uint8)
+
+
+def _sum16(a: np.ndarray) -> np.ndarray:
+    """Sum of big-endian 16-bit words of each row (odd length: last byte << 8)."""
+    a = a.astype(np.uint64)
+    if a.shape[1] % 2:
+        a = np.concatenate([a, np.zeros((a.shape[0], 1), np.uint64)], axis=1)
+    return ((a[:, 0::2] << np.uint64(8)) | a[:, 1::2]).sum(axis=1)
+
+
+def _fold_not(s: np.ndarray) -> np.ndarray:
+    s = s.astype(np.uint64)
+    s = s & np.uint64(0xFFFFFFFF)  # the reference accumulates in uint32
+    while np.any(s > 0xFFFF):
+        s = np.where(s > 0xFFFF, (s >> np.uint64(16)) + (s & np.uint64(0xFFFF)), s)
+    return (~s.astype(np.uint16)).astype(np.uint16)
+
+
+def _ip4_header(a: np.ndarray, c: int, length: np.ndarray, ident: np.ndarray, ttl: np.ndarray,
+                proto: int, src: np.ndarray, dst: np.ndarray) -> None:
+    a[:, c] = 0x45
+    a[:, c + 1] = 0
+    _be16(a, c + 2, length)
+    _be16(a, c + 4, ident)
+    a[:, c + 6] = 0x40  # DF
+    a[:, c + 7] = 0
+    a[:, c + 8] = ttl
+    a[:, c + 9] = proto
+    a[:, c + 10:c + 12] = 0
+    _be32(a, c + 12, src)
+    _be32(a, c + 16, dst)
+    cs = _fold_not(_sum16(a[:, c:c + 20]))
+    _be16(a, c + 10, cs)
+
+
+def _l4_checksum(a: np.ndarray, ip: int, l4: int, seg_len: int, proto: int, col: int) -> None:
+    """Valid TCP/UDP checksum (tcpip.go:26-88) for rows whose segment is a[:, l4:l4+seg_len]."""
+    a[:, l4 + col:l4 + col + 2] = 0
+    s = _sum16(a[:, ip + 12:ip + 20]) + np.uint64(proto) + np.uint64(seg_len & 0xFFFF) + \
+        np.uint64(seg_len >> 16) + _sum16(a[:, l4:l4 + seg_len])
+    _be16(a, l4 + col, _fold_not(s))
+
+
+def _corrupt(a: np.ndarray, rows: np.ndarray, col: int) -> None:
+    a[rows, col] ^= 0x5A
+
+
+def _rand_bytes(seed: int, stream: int, n: int, width: int, base: int = 0) -> np.ndarray:
+    """(n, width) random bytes from splitmix64 stream `stream` (rows base .. base+n)."""
+    w = (width + 7) // 8
+    return splitmix64(seed, n * w, stream, base * w).view(np.uint8).reshape(n, w * 8)[:, :width]
+
+
+def _udp64_rows(a: np.ndarray, seed: int, base: int, free: np.ndarray) -> None:
+    n = a.shape[0]
+    r = [splitmix64(seed, n, k, base) for k in range(4)]
+    a[:, 0:12] = _rand_bytes(seed, 100, n, 12, base) & 0xFE  # unicast MACs
+    _be16(a, 12, np.full(n, 0x0800))
+    src = (r[1] & np.uint64(0xFFFFFFFF)).astype(np.uint64)
+    dst = (r[1] >> np.uint64(32)).astype(np.uint64)
+    ident = (r[2] & np.uint64(0xFFFF)).astype(np.int64)
+    ttl = ((r[2] >> np.uint64(16)) & np.uint64(0xFF)).astype(np.uint8) | 1
+    _ip4_header(a, 14, np.full(n, 50), ident, ttl, 17, src, dst)
+    _be16(a, 34, _pick(free, r[3]))
+    _be16(a, 36, _pick(free, r[3] >> np.uint64(32)))
+    _be16(a, 38, np.full(n, 30))
+    a[:, 42:64] = _rand_bytes(seed, 101, n, 22, base)
+    _l4_checksum(a, 14, 34, 30, 17, 6)
+    bad = np.nonzero(((np.arange(n) + base) % 64) == 63)[0]
+    _corrupt(a, bad, 24)  # IPv4 header checksum byte
+
+
+def make_udp64(n: int, seed: int = 0x5EED0002, chunk: int = 1 << 20) -> PacketBatch:
+    """Config 2: 64 B Eth/IPv4/UDP (IHL 5, Length 50, UDP Length 30)."""
+    data = np.zeros(n * 64 + PAD, dtype=np.uint8)
+    rows = data[: n * 64].reshape(n, 64)
+    free = _free_ports(TABLES.udp_port)
+    for c0 in range(0, n, chunk):
+        a = np.zeros((min(chunk, n - c0), 64), dtype=np.uint8)
+        _udp64_rows(a, seed, c0, free)
+        rows[c0:c0 + a.shape[0]] = a
+    return PacketBatch(data, n * 64, (np.arange(n, dtype=np.uint64) * 64).astype(np.uint32),
+                       np.full(n, 64, dtype=np.uint32))
+
+
+IMIX_SIZES = (64, 576, 1500)
+IMIX_WEIGHTS = (7, 4, 1)
+
+
+def _tcp_frames(n: int, size: int, r: list, opts: np.ndarray, vlan: bool, free: np.ndarray,
+                bad: np.ndarray, seed: int, stream: int) -> np.ndarray:
+    """n Eth(/Dot1Q)/IPv4/TCP frames of `size` bytes; rows in `opts` carry NOP,NOP,TS."""
+    a = np.zeros((n, size), dtype=np.uint8)
+    a[:, 0:12] = _rand_bytes(seed, stream, n, 12) & 0xFE
+    c = 12
+    if vlan:
+        _be16(a, 12, np.full(n, 0x8100))
+        _be16(a, 14, (r[5] & np.uint64(0x0FFF)).astype(np.int64))
+        c = 16
+    _be16(a, c, np.full(n, 0x0800))
+    ip = c + 2
+    l4 = ip + 20
+    seg = size - l4
+    src = (r[1] & np.uint64(0xFFFFFFFF)).astype(np.uint64)
+    dst = (r[1] >> np.uint64(32)).astype(np.uint64)
+    ident = (r[2] & np.uint64(0xFFFF)).astype(np.int64)
+    ttl = ((r[2] >> np.uint64(16)) & np.uint64(0xFF)).astype(np.uint8) | 1
+    _ip4_header(a, ip, np.full(n, size - ip), ident, ttl, 6, src, dst)
+    _be16(a, l4, _pick(free, r[3]))
+    _be16(a, l4 + 2, _pick(free, r[3] >> np.uint64(32)))
+    _be32(a, l4 + 4, r[4] & np.uint64(0xFFFFFFFF))
+    _be32(a, l4 + 8, r[4] >> np.uint64(32))
+    a[:, l4 + 12] = 0x50
+    a[:, l4 + 13] = 0x10 | (((r[2] >> np.uint64(24)) & np.uint64(1)).astype(np.uint8) << 3)  # ACK(+PSH)
+    _be16(a, l4 + 14, ((r[2] >> np.uint64(32)) & np.uint64(0xFFFF)).astype(np.int64))
+    if seg > 20:
+        body = _rand_bytes(seed, stream + 1, n, seg - 20)
+        a[:, l4 + 20:] = body
+    if len(opts):
+        a[opts, l4 + 12] = 0x80
+        a[opts, l4 + 20] = 1
+        a[opts, l4 + 21] = 1
+        a[opts, l4 + 22] = 8
+        a[opts, l4 + 23] = 10
+    _l4_checksum(a, ip, l4, seg, 6, 16)
+    _corrupt(a, bad, l4 + 16)
+    return a
+
+
+def make_imix(n: int, seed: int = 0x5EED0003, vlan: bool = True, align: int = 16,
+              chunk: int = 16384) -> PacketBatch:
+    """Config 3: IMIX 64/576/1500 B (7:4:1), Eth/Dot1Q/IPv4/TCP, seeded shuffle.
+
+    3 in 10 of the 576/1500 B packets (1/8 of all) carry NOP,NOP,Timestamp options
+    (doff 8); a 64 B frame has no room for them.  Packet starts are `align`-aligned.
+    """
+    wsum = sum(IMIX_WEIGHTS)
+    cls = np.repeat(np.arange(3), [n * w // wsum for w in IMIX_WEIGHTS])
+    cls = np.concatenate([cls, np.zeros(n - len(cls), dtype=cls.dtype)])
+    perm = np.argsort(splitmix64(seed, n, 99), kind="stable")
+    cls = cls[perm]
+    sizes = np.array(IMIX_SIZES, dtype=np.int64)[cls]
+    slot = (sizes + align - 1) // align * align
+    offs = np.zeros(n, dtype=np.int64)
+    if n > 1:
+        np.cumsum(slot[:-1], out=offs[1:])
+    total = int(offs[-1] + sizes[-1]) if n else 0
+    data = np.zeros(total + PAD, dtype=np.uint8)
+    free = _free_ports(TABLES.tcp_port)
+    gidx = np.arange(n)
+    bad_all = (gidx % 64) == 63
+    ropt = splitmix64(seed, n, 98)
+    opt_all = (cls > 0) & ((ropt % np.uint64(10)) < np.uint64(3))
+    for k, size in enumerate(IMIX_SIZES):
+        rows_all = np.nonzero(cls == k)[0]
+        for c0 in range(0, len(rows_all), chunk):
+            rows = rows_all[c0:c0 + chunk]
+            m = len(rows)
+            r = [splitmix64(seed + c0, m, 16 * k + j) for j in range(6)]
+            opts = np.nonzero(opt_all[rows])[0]
+            bad = np.nonzero(bad_all[rows])[0]
+            frames = _tcp_frames(m, size, r, opts, vlan, free, bad, seed + c0, 200 + 2 * k)
+            idx = offs[rows][:, None] + np.arange(size)[None, :]
+            data[idx.reshape(-1)] = frames.reshape(-1)
+    return PacketBatch(data, total, offs.astype(np.uint32), sizes.astype(np.uint32))
+
+
+def make_vxlan(n: int, seed: int = 0x5EED0004) -> PacketBatch:
+    """Config 4: 128 B Eth/IPv4/UDP(4789)/VXLAN/Eth/IPv4/TCP (104 B of headers + 24 B payload)."""
+    a = np.zeros((n, 128), dtype=np.uint8)
+    r = [splitmix64(seed, n, k) for k in range(10)]
+    free_u = _free_ports(TABLES.udp_port)
+    free_t = _free_ports(TABLES.tcp_port)
+    a[:, 0:12] = _rand_bytes(seed, 100, n, 12) & 0xFE
+    _be16(a, 12, np.full(n, 0x0800))
+    _ip4_header(a, 14, np.full(n, 114), (r[1] & np.uint64(0xFFFF)).astype(np.int64),
+                np.full(n, 64, np.uint8), 17, (r[2] & np.uint64(0xFFFFFFFF)),
+                (r[2] >> np.uint64(32)))
+    _be16(a, 34, _pick(free_u, r[3]))
+    _be16(a, 36, np.full(n, 4789))
+    _be16(a, 38, np.full(n, 94))
+    a[:, 42] = 0x08  # VXLAN I flag
+    _be32(a, 46, (r[4] & np.uint64(0xFFFFFF)) << np.uint64(8))
+    a[:, 50:62] = _rand_bytes(seed, 101, n, 12) & 0xFE
+    _be16(a, 62, np.full(n, 0x0800))
+    ttl = ((r[6] >> np.uint64(16)) & np.uint64(0xFF)).astype(np.uint8) | 1
+    _ip4_header(a, 64, np.full(n, 64), (r[6] & np.uint64(0xFFFF)).astype(np.int64), ttl, 6,
+                (r[7] & np.uint64(0xFFFFFFFF)), (r[7] >> np.uint64(32)))
+    _be16(a, 84, _pick(free_t, r[8]))
+    _be16(a, 86, _pick(free_t, r[8] >> np.uint64(32)))
+    _be32(a, 88, r[9] & np.uint64(0xFFFFFFFF))
+    _be32(a, 92, r[9] >> np.uint64(32))
+    a[:, 96] = 0x50
+    a[:, 97] = 0x18
+    _be16(a, 98, np.full(n, 0x2000))
+    a[:, 104:128] = _rand_bytes(seed, 102, n, 24)
+    _l4_checksum(a, 64, 84, 44, 6, 16)
+    # outer UDP checksum 0 ("not computed"), as VXLAN encapsulators commonly send
+    bad = np.nonzero((np.arange(n) % 64) == 63)[0]
+    _corrupt(a, bad, 84 + 16)
+    data = np.zeros(n * 128 + PAD, dtype=np.uint8)
+    data[: n * 128] = a.reshape(-1)
+    return PacketBatch(data, n * 128, (np.arange(n, dtype=np.uint64) * 128).astype(np.uint32),
+                       np.full(n, 128, dtype=np.uint32))
+
+
+def make_mixed(n: int, seed: int = 0x5EED0005) -> PacketBatch:
+    """A mixed batch (the three configurations interleaved) for parity tests."""
+    parts = [make_udp64(n // 3 + 1, seed), make_imix(n // 3 + 1, seed + 1), make_vxlan(n // 3 + 1, seed + 2)]
+    pkts = []
+    for k in range(n):
+        b = parts[k % 3]
+        pkts.append(b.packet(k // 3))
+    return PacketBatch.from_packets(pkts)

@@ -1,0 +1,146 @@
+"""Load tests/golden/golden.json and check a BatchResult against its expectations.
+
+Shared by the oracle pinning tests (CPU) and the device parity tests (GPU).
+"""
+from __future__ import annotations
+
+import json
+import os
+import struct
+
+from gopacket_amd.batch import PacketBatch
+from gopacket_amd.layers import LAYERTYPE_NAMES
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLDEN = os.path.join(HERE, "golden", "golden.json")
+
+NAME_TO_LT = {v: k for k, v in LAYERTYPE_NAMES.items()}
+DEC_BITS = {"Ethernet": 1, "Dot1Q": 2, "IPv4": 4, "IPv6": 8, "IPv6ExtensionSkipper": 16, "TCP": 32,
+            "UDP": 64, "VXLAN": 128, "Payload": 256, "Fragment": 512}
+
+
+def load():
+    with open(GOLDEN) as f:
+        return json.load(f)
+
+
+def case_bytes(c) -> bytes:
+    b = bytes.fromhex(c["hex"])
+    if "tail_repeat" in c:
+        b += bytes.fromhex(c["tail_repeat"]["hex"]) * c["tail_repeat"]["count"]
+    drop = c["expect"].get("drop_last", 0)
+    return b[:len(b) - drop] if drop else b
+
+
+def case_config(c):
+    first = NAME_TO_LT[c["first"]]
+    mask = 0
+    for d in c["decoders"]:
+        mask |= DEC_BITS[d]
+    options = 1 if c["ignore_unsupported"] else 0
+    return first, mask, options
+
+
+def single_batch(c) -> PacketBatch:
+    return PacketBatch.from_packets([case_bytes(c)])
+
+
+def _ipv4_options(pkt: bytes, c0: int, c1: int):
+    """Option list (type, length) of an IPv4 header, walked like ip4.go:240-273."""
+    out, o = [], c0 + 20
+    pad = b""
+    while o < c1:
+        t = pkt[o]
+        if t == 0:
+            out.append([0, 1])
+            pad = pkt[o + 1:c1]
+            break
+        if t == 1:
+            out.append([1, 1])
+            o += 1
+            continue
+        out.append([t, pkt[o + 1]])
+        o += pkt[o + 1]
+    return out, pad
+
+
+def _tcp_options(pkt: bytes, c0: int, c1: int):
+    out, o = [], c0 + 20
+    while o < c1:
+        k = pkt[o]
+        if k == 0:
+            out.append([0, 1])
+            break
+        if k == 1:
+            out.append([1, 1])
+            o += 1
+            continue
+        out.append([k, pkt[o + 1]])
+        o += pkt[o + 1]
+    return out
+
+
+def check(c, res, i: int = 0, pkt: bytes | None = None) -> None:
+    """Assert result row i against the case's expectations."""
+    e = c["expect"]
+    name = c["name"]
+    want = [NAME_TO_LT[x] for x in e["decoded"]]
+    assert res.decoded(i) == want, f"{name}: decoded {res.decoded(i)} != {want}"
+    err = res.err(i)
+    if e["err"] is None:
+        assert err is None, f"{name}: unexpected error {err}"
+    else:
+        assert err is not None and str(err) == e["err"], f"{name}: error {err!r} != {e['err']!r}"
+    assert res.truncated(i) == e["truncated"], f"{name}: truncated {res.truncated(i)}"
+    if "stop" in e:
+        assert res.stop_type(i) == e["stop"], f"{name}: stop {res.stop_type(i)}"
+    if "ip4_csum" in e:
+        assert res.ip4_checksum(i) == e["ip4_csum"], f"{name}: ip4 csum {res.ip4_checksum(i):#x}"
+    if "l4_csum" in e:
+        assert res.l4_checksum(i) == e["l4_csum"], f"{name}: l4 csum {res.l4_checksum(i)}"
+    if pkt is None:
+        pkt = case_bytes(c)
+    for obj, key in (("IPv4", "ipv4"), ("TCP", "tcp"), ("UDP", "udp"), ("IPv6", "ipv6"),
+                     ("Dot1Q", "dot1q"), ("VXLAN", "vxlan")):
+        if key not in e or res.ext is None:
+            continue
+        rng = res.layer(i, obj)
+        assert rng is not None, f"{name}: no {obj} object"
+        (c0, c1), (p0, p1) = rng
+        f = e[key]
+        if "contents" in f:
+            assert [c0, c1] == f["contents"], f"{name}: {obj} contents {(c0, c1)}"
+        if "payload" in f:
+            assert [p0, p1] == f["payload"], f"{name}: {obj} payload {(p0, p1)}"
+        h = pkt[c0:c1]
+        if obj == "IPv4":
+            if "Length" in f:
+                assert struct.unpack(">H", h[2:4])[0] == f["Length"]
+                assert struct.unpack(">H", h[4:6])[0] == f["Id"]
+                assert h[6] >> 5 == f["Flags"] and h[8] == f["TTL"] and h[9] == f["Protocol"]
+                assert struct.unpack(">H", h[10:12])[0] == f["Checksum"]
+                assert ".".join(map(str, h[12:16])) == f["SrcIP"]
+                assert ".".join(map(str, h[16:20])) == f["DstIP"]
+            if "options" in f:
+                opts, pad = _ipv4_options(pkt, c0, c1)
+                assert opts == f["options"], f"{name}: options {opts}"
+                assert pad.hex() == f["padding"], f"{name}: padding {pad.hex()}"
+        if obj == "TCP":
+            if "SrcPort" in f:
+                sp, dp, seq, ack = struct.unpack(">HHII", h[:12])
+                assert (sp, dp, seq, ack) == (f["SrcPort"], f["DstPort"], f["Seq"], f["Ack"])
+                assert h[12] >> 4 == f["DataOffset"]
+                assert struct.unpack(">H", h[14:16])[0] == f["Window"]
+                assert struct.unpack(">H", h[16:18])[0] == f["Checksum"]
+            if "options" in f:
+                assert _tcp_options(pkt, c0, c1) == f["options"]
+        if obj == "UDP" and "SrcPort" in f:
+            assert struct.unpack(">HHHH", h[:8]) == (f["SrcPort"], f["DstPort"], f["Length"], f["Checksum"])
+        if obj == "Dot1Q":
+            assert (struct.unpack(">H", h[:2])[0] & 0x0FFF) == f["VLANIdentifier"]
+            assert h[0] >> 5 == f["Priority"] and bool(h[0] & 0x10) == f["DropEligible"]
+        if obj == "VXLAN":
+            assert int.from_bytes(h[4:7], "big") == f["VNI"] and bool(h[0] & 0x08) == f["ValidIDFlag"]
+    if "inner_ipv4_contents" in e and res.ext is not None:
+        (c0, c1), _ = res.layer(i, "IPv4")
+        assert [c0, c1] == e["inner_ipv4_contents"], f"{name}: A11 inner IPv4 {(c0, c1)}"

@@ -1,0 +1,225 @@
+"""Device parity: the HIP path (through the C-ABI) vs the CPU oracle, bit-exact.
+
+Every output word is compared: status, layers, both FastHashes, both checksums
+and (with ext) the decoded list, error arguments and every layer object's
+contents/payload ranges.  Cases: the reference's golden vectors, the synthetic
+BASELINE configurations, exhaustive truncations and seeded byte mutations of the
+golden packets, odd batch layouts (unaligned / shuffled offsets, packets larger
+than an LDS window, empty packets) and mutated dispatch tables.
+"""
+import numpy as np
+import pytest
+
+import golden_cases as G
+import oracle_ref as O
+from gopacket_amd import layers as L
+from gopacket_amd import synth
+from gopacket_amd.batch import PacketBatch
+
+pytestmark = pytest.mark.gpu
+
+ALL = 0x3FF
+
+
+def _parser(first=L.LayerTypeEthernet, mask=ALL, options=0, tables=None):
+    from gopacket_amd import parser as P
+    p = P.DecodingLayerParser(first)
+    p._mask = mask
+    p.IgnoreUnsupported = bool(options & 1)
+    p.ComputeChecksums = not (options & 256)
+    p.ComputeFlowHashes = not (options & 512)
+    if tables is not None:
+        p._tables = tables.copy()
+    return p
+
+
+def assert_same(dev, ref, batch=None, ext=True):
+    for f in ("status", "layers", "net_hash", "tp_hash", "csum"):
+        a, b = getattr(dev, f), getattr(ref, f)
+        bad = np.nonzero(a != b)[0]
+        if len(bad):
+            i = int(bad[0])
+            pk = batch.packet(i).hex() if batch is not None else "?"
+            raise AssertionError(
+                f"{f} differs at {len(bad)} packets; first i={i}: dev={int(a[i]):#x} ref={int(b[i]):#x} "
+                f"dev_decoded={dev.decoded(i) if f != 'layers' else '-'} ref_decoded={ref.decoded(i)} "
+                f"pkt={pk[:200]}")
+    if ext:
+        a = dev.ext.view(np.uint8).reshape(len(dev), -1)
+        b = ref.ext.view(np.uint8).reshape(len(ref), -1)
+        bad = np.nonzero(np.any(a != b, axis=1))[0]
+        if len(bad):
+            i = int(bad[0])
+            raise AssertionError(f"ext differs at {len(bad)} packets; first i={i}: dev={dev.ext[i]} "
+                                 f"ref={ref.ext[i]}")
+
+
+def run_both(batch, first=L.LayerTypeEthernet, mask=ALL, options=0, tables=None, ext=True):
+    dev = _parser(first, mask, options, tables).DecodeBatch(batch, ext=ext)
+    ref = O.decode(batch, first, mask, options, tables=tables, ext=ext, nthreads=8)
+    assert_same(dev, ref, batch, ext)
+    return dev
+
+
+META = G.load()
+CASES = META["cases"]
+
+
+@pytest.mark.parametrize("c", CASES, ids=[c["name"] for c in CASES])
+def test_golden_case_on_device(c):
+    first, mask, opts = G.case_config(c)
+    dev = run_both(G.single_batch(c), first, mask, opts)
+    G.check(c, dev)
+
+
+def _golden_packets():
+    return [G.case_bytes(c) for c in CASES]
+
+
+@pytest.mark.parametrize("first", [L.LayerTypeEthernet, L.LayerTypeIPv4, L.LayerTypeIPv6,
+                                   L.LayerTypeTCP, L.LayerTypeDot1Q, 999])
+@pytest.mark.parametrize("mask", [ALL, 0x1 | 0x4 | 0x20 | 0x100, 0x1 | 0x2 | 0x4 | 0x40 | 0x80,
+                                  0x1 | 0x8 | 0x10 | 0x40 | 0x200])
+def test_golden_batch_configs(first, mask):
+    run_both(PacketBatch.from_packets(_golden_packets()), first, mask, 0)
+    run_both(PacketBatch.from_packets(_golden_packets()), first, mask, 1)
+
+
+def _mutations(seed=7, per_packet=400):
+    rng = np.random.default_rng(seed)
+    out = []
+    for p in _golden_packets():
+        p = p[:2048]
+        # every truncation
+        out += [p[:k] for k in range(len(p) + 1)]
+        # byte flips and header-field fuzz in the first 128 bytes
+        a = np.frombuffer(p, np.uint8)
+        for _ in range(per_packet):
+            b = a.copy()
+            k = rng.integers(1, 6)
+            pos = rng.integers(0, min(len(b), 128), size=k)
+            b[pos] = rng.integers(0, 256, size=k, dtype=np.uint8)
+            out.append(b.tobytes()[: rng.integers(len(b) // 2, len(b) + 1)])
+    return out
+
+
+@pytest.mark.parametrize("options", [0, 1])
+def test_fuzz_truncations_and_mutations(options):
+    pk = _mutations()
+    b = PacketBatch.from_packets(pk)
+    run_both(b, L.LayerTypeEthernet, ALL, options)
+    run_both(b, L.LayerTypeIPv4, 0x4 | 0x20 | 0x40 | 0x100, options)
+
+
+def test_fuzz_random_headers():
+    """Random bytes behind valid-looking Ethernet/IPv4/IPv6 prefixes: exercises option walks,
+    HBH/jumbogram paths and every error site."""
+    rng = np.random.default_rng(11)
+    pkts = []
+    for k in range(20000):
+        n = int(rng.integers(0, 200))
+        body = rng.integers(0, 256, size=n, dtype=np.uint8).tobytes()
+        kind = k % 6
+        if kind == 0:
+            pkts.append(b"\x00" * 12 + b"\x08\x00" + bytes([0x40 | rng.integers(0, 16)]) + body)
+        elif kind == 1:
+            pkts.append(b"\x00" * 12 + b"\x86\xdd" + b"\x60\x00\x00\x00" + body[:2] + b"\x00" + body)
+        elif kind == 2:
+            pkts.append(b"\x00" * 12 + b"\x81\x00" + body)
+        elif kind == 3:
+            pkts.append(b"\x00" * 12 + b"\x88\xa8" + b"\x00\x01\x81\x00" + body)
+        elif kind == 4:
+            pkts.append(b"\x00" * 12 + bytes([rng.integers(0, 8), rng.integers(0, 256)]) + body)
+        else:
+            pkts.append(body)
+    run_both(PacketBatch.from_packets(pkts), L.LayerTypeEthernet, ALL, 0)
+
+
+@pytest.mark.parametrize("maker", [synth.make_udp64, synth.make_imix, synth.make_vxlan, synth.make_mixed])
+def test_synthetic_configs(maker):
+    b = maker(1 << 15)
+    run_both(b, ext=True)
+    run_both(b, ext=False)
+
+
+def test_layouts_unaligned_shuffled_large_empty():
+    pk = _golden_packets() + [b"", b"\x01", b"\x00" * 13]
+    big = [G.case_bytes(c) for c in CASES if c["name"] == "ipv6_jumbogram_dlp"][0]
+    pk += [big, big[:20000], big + big[:5000]]
+    pk = pk * 5
+    # unaligned packed layout
+    b = PacketBatch.from_packets(pk, align=1)
+    run_both(b)
+    # shuffled (non-monotonic) offsets over the same buffer
+    perm = np.random.default_rng(3).permutation(b.n)
+    b2 = PacketBatch(b.data, b.data_len, b.offset[perm].copy(), b.caplen[perm].copy())
+    run_both(b2)
+    # n not a multiple of 64, single packet
+    run_both(PacketBatch.from_packets(pk[:65]))
+    run_both(PacketBatch.from_packets(pk[:1]))
+
+
+def test_mutated_dispatch_tables():
+    t = L.DispatchTables()
+    t.udp_port[9999] = L.LayerTypeVXLAN       # RegisterUDPPortLayerType(9999, VXLAN)
+    t.tcp_port[80] = L.LayerTypeIPv4          # a deliberately odd registration
+    t.ethertype[0x0800] = L.LayerTypeIPv6     # EthernetTypeMetadata override
+    t.ipproto[6] = L.LayerTypeUDP
+    pk = _golden_packets() + [synth.make_vxlan(64).packet(k) for k in range(64)]
+    run_both(PacketBatch.from_packets(pk), tables=t)
+
+
+def test_options_no_checksums_no_hashes():
+    b = synth.make_mixed(3000)
+    for opt in (256, 512, 768, 769):
+        run_both(b, options=opt)
+
+
+def test_host_path_matches_device_path():
+    from gopacket_amd import parser as P
+    b = synth.make_mixed(5000)
+    p = P.DecodingLayerParser(L.LayerTypeEthernet)
+    p._mask = ALL
+    dev = p.DecodeBatch(b, ext=True)
+    host = p.DecodeBatchHost(b, ext=True)
+    assert_same(host, dev, b)
+
+
+def test_decode_layers_single_packet_api():
+    from gopacket_amd import parser as P
+    c = [c for c in CASES if c["name"] == "simple_tcp_dlp4"][0]
+    p = P.NewDecodingLayerParser(L.LayerTypeEthernet, P.Ethernet(), P.IPv4(), P.TCP(), P.Payload())
+    decoded = []
+    err = p.DecodeLayers(G.case_bytes(c), decoded)
+    assert err is None and decoded == [17, 20, 44, 2] and not p.Truncated
+    c = [c for c in CASES if c["name"] == "udp_truncated"][0]
+    p2 = P.NewDecodingLayerParser(L.LayerTypeEthernet, P.Ethernet(), P.Dot1Q(), P.IPv4(), P.UDP(),
+                                  P.Payload())
+    err = p2.DecodeLayers(G.case_bytes(c), decoded)
+    assert err is None and p2.Truncated and decoded == [17, 15, 20, 45, 2]
+
+
+def test_full_size_config2_properties():
+    """BASELINE config 2 at full size (2^24 packets): size-independent properties, plus a
+    bit-exact oracle comparison on a strided sample."""
+    import torch
+    from gopacket_amd import parser as P
+    n = 1 << 24
+    b = synth.make_udp64(n)
+    p = P.DecodingLayerParser(L.LayerTypeEthernet)
+    p._mask = ALL
+    res = p.DecodeBatch(b, ext=False)
+    assert np.all(res.status & 3 == 0)
+    assert np.all(((res.status >> 4) & 31) == 4)
+    bad = (np.arange(n) % 64) == 63
+    stored = (b.data[24:n * 64:64].astype(np.uint32) << 8) | b.data[25:n * 64:64]
+    assert np.array_equal((res.csum & 0xFFFF) == stored, ~bad)
+    assert np.all(res.csum >> 16 == 0)
+    # sample
+    idx = np.arange(0, n, 4099)
+    sb = PacketBatch(b.data, b.data_len, b.offset[idx].copy(), b.caplen[idx].copy())
+    ref = O.decode(sb, ext=False, nthreads=8)
+    for f in ("status", "layers", "net_hash", "tp_hash", "csum"):
+        assert np.array_equal(getattr(res, f)[idx], getattr(ref, f)), f
+    del res
+    torch.cuda.empty_cache()
