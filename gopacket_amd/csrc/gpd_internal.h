@@ -7,14 +7,27 @@
 
 namespace gpd {
 
-// Device dispatch tables: a two-level page structure per 16-bit table.
-//   words [0,256)      ipproto -> LayerType
-//   words [256,512)    ethertype high byte -> page
-//   words [512,768)    tcp port high byte  -> page
-//   words [768,1024)   udp port high byte  -> page
-//   words [1024, ...)  pages of 256 LayerTypes; page 0 is all zero
-// The reference's tables are 3 x 64K + 256 entries (≈384 KB); with its defaults this
-// structure is ≈9 KB, small enough for every lookup to hit L1/L2.
+// ---- device dispatch tables ---------------------------------------------------------
+// Two encodings of the same four reference tables (ethertype[65536], ipproto[256],
+// tcp_port[65536], udp_port[65536]; layers/enums.go:304-345, layers/ports.go:62-122):
+//
+// (a) HASH (default, copied into LDS by every workgroup): the tables are sparse (the
+//     reference defaults hold 18 + 11 + 16 nonzero 16-bit entries), so each 64K table
+//     is an open-addressed hash of its nonzero entries, u32 slots {key:16 | value:16}
+//     (value 0 never stored => an empty slot ends the probe).  Layout in u32 words:
+//       [0,32)                     type LUT: byte t = decoder id | code << 4 for t < 128
+//                                  (decoder id 15 = not registered)
+//       [32,160)                   ipproto -> LayerType (u16 pairs)
+//       [eth_base, +2^eth_bits)    ethertype hash
+//       [tcp_base, +2^tcp_bits)    tcp port hash
+//       [udp_base, +2^udp_bits)    udp port hash
+// (b) PAGES (fallback when a table is too dense for the LDS budget): the image holds only
+//     the LUT and ipproto; the 64K tables are two-level pages in global memory, u16 words:
+//     [256,512) eth dir, [512,768) tcp dir, [768,1024) udp dir, then 256-entry pages
+//     (page 0 = zeros).
+constexpr uint32_t kHashLutWords = 32;
+constexpr uint32_t kHashProtoWords = 128;
+constexpr uint32_t kHashMaxWords = 4096;  // 16 KB cap for the LDS image
 constexpr uint32_t kTabIpProto = 0;
 constexpr uint32_t kTabEthDir = 256;
 constexpr uint32_t kTabTcpDir = 512;
@@ -33,14 +46,24 @@ struct KParams {
   uint64_t *tp_hash;
   uint32_t *csum;
   gpd_ext_rec *ext;
-  const uint16_t *tables;
+  const uint32_t *image;       // LUT + ipproto (+ hash tables in HASH mode); staged into LDS
+  const uint16_t *pages;       // PAGES mode: two-level page tables in global memory
+  uint32_t image_words;
+  uint32_t use_pages;          // 1 => 64K lookups go to `pages`
+  uint32_t eth_base, tcp_base, udp_base;  // word offsets of the hashes inside `image`
+  uint32_t eth_bits, tcp_bits, udp_bits;  // log2 of each hash's slot count
   uint32_t first;
   uint32_t decoders;
   uint32_t options;
-  uint32_t pad;
+  uint32_t stage;              // LDS window bytes per buffer (chosen by the runtime)
 };
 
 // Launch the decode kernel over P (asynchronous on `stream`).
 hipError_t launch_decode(const KParams &P, hipStream_t stream, int num_cus);
+
+// Fibonacci hash of a 16-bit key into 2^bits slots (host and device must agree).
+__host__ __device__ inline uint32_t key_hash(uint32_t key, uint32_t bits) {
+  return ((key * 40503u) & 0xFFFFu) >> (16 - bits);
+}
 
 }  // namespace gpd

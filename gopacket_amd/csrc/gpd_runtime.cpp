@@ -87,6 +87,41 @@ std::vector<uint16_t> encode_tables(const uint16_t *eth, const uint16_t *proto,
   return out;
 }
 
+// Decoder id per LayerType for the registered set (the DecodingLayerMap of parser.go:147-164,
+// filled from each decoder's CanDecode, layertypes.go:193-198 for the extension class) and
+// the 4-bit code the `layers` word uses for it (include/gpd.h GPD_C_*).
+void type_lut(uint32_t decoders, uint8_t lut[128]) {
+  struct E { uint32_t lt, dec, code; };
+  static const E kMap[] = {{17, 0, 1},  {15, 1, 2},  {20, 2, 3},  {21, 3, 4},  {46, 4, 5},
+                           {47, 4, 6},  {48, 4, 7},  {49, 4, 8},  {44, 5, 9},  {45, 6, 10},
+                           {116, 7, 11}, {2, 8, 12}, {3, 9, 13}};
+  memset(lut, 0xFF, 128);
+  for (const E &e : kMap)
+    if (decoders & (1u << e.dec)) lut[e.lt] = (uint8_t)(e.dec | (e.code << 4));
+}
+
+// Open-addressed hash of the nonzero entries of a 64K table; returns log2(slots) or 0 if it
+// would not fit `max_slots` with every probe sequence <= 8.
+uint32_t build_hash(const uint16_t *t, uint32_t max_slots, std::vector<uint32_t> &slots) {
+  std::vector<uint32_t> keys;
+  for (uint32_t k = 0; k < 65536; k++)
+    if (t[k]) keys.push_back(k);
+  for (uint32_t bits = 4; (1u << bits) <= max_slots && bits <= 16; bits++) {
+    const uint32_t n = 1u << bits, mask = n - 1;
+    if (keys.size() * 2 > n) continue;
+    slots.assign(n, 0);
+    bool ok = true;
+    for (uint32_t k : keys) {
+      uint32_t h = gpd::key_hash(k, bits), probe = 0;
+      while (slots[h]) { h = (h + 1) & mask; probe++; }
+      if (probe >= 8) { ok = false; break; }
+      slots[h] = (k << 16) | t[k];
+    }
+    if (ok) return bits;
+  }
+  return 0;
+}
+
 }  // namespace
 
 struct gpd_ctx {
@@ -95,8 +130,10 @@ struct gpd_ctx {
   uint32_t first = GPD_LT_ETHERNET;
   uint32_t decoders = GPD_DEC_ALL;
   uint32_t options = 0;
-  uint16_t *d_tables = nullptr;
-  size_t tables_words = 0;
+  uint32_t *d_image = nullptr;  // LUT + ipproto (+ hashes)
+  uint16_t *d_pages = nullptr;  // PAGES fallback
+  uint32_t image_words = 0, use_pages = 0;
+  uint32_t eth_base = 0, tcp_base = 0, udp_base = 0, eth_bits = 0, tcp_bits = 0, udp_bits = 0;
   bool timing = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
@@ -137,18 +174,35 @@ int gpd_ctx_reload_tables(gpd_ctx *ctx, const gpd_config *cfg) {
   if (cfg->ipproto) std::memcpy(proto.data(), cfg->ipproto, 256 * 2);
   if (cfg->tcp_port) std::memcpy(tcp.data(), cfg->tcp_port, 65536 * 2);
   if (cfg->udp_port) std::memcpy(udp.data(), cfg->udp_port, 65536 * 2);
-  std::vector<uint16_t> blob = encode_tables(eth.data(), proto.data(), tcp.data(), udp.data());
+  // LDS image: LUT (32 words) + ipproto (128 words) + the three hashes
+  std::vector<uint32_t> img(gpd::kHashLutWords + gpd::kHashProtoWords, 0);
+  type_lut(ctx->decoders, reinterpret_cast<uint8_t *>(img.data()));
+  std::memcpy(img.data() + gpd::kHashLutWords, proto.data(), 256 * sizeof(uint16_t));
+  std::vector<uint32_t> he, ht, hu;
+  const uint32_t room = gpd::kHashMaxWords - (uint32_t)img.size();
+  uint32_t be = build_hash(eth.data(), room / 2, he);
+  uint32_t bt = be ? build_hash(tcp.data(), room / 4, ht) : 0;
+  uint32_t bu = bt ? build_hash(udp.data(), room / 4, hu) : 0;
   HIP_TRY(hipSetDevice(ctx->device));
-  if (ctx->d_tables && ctx->tables_words < blob.size()) {
-    HIP_TRY(hipFree(ctx->d_tables));
-    ctx->d_tables = nullptr;
+  if (ctx->d_image) { HIP_TRY(hipFree(ctx->d_image)); ctx->d_image = nullptr; }
+  if (ctx->d_pages) { HIP_TRY(hipFree(ctx->d_pages)); ctx->d_pages = nullptr; }
+  if (be && bt && bu) {
+    ctx->use_pages = 0;
+    ctx->eth_base = (uint32_t)img.size(); ctx->eth_bits = be;
+    img.insert(img.end(), he.begin(), he.end());
+    ctx->tcp_base = (uint32_t)img.size(); ctx->tcp_bits = bt;
+    img.insert(img.end(), ht.begin(), ht.end());
+    ctx->udp_base = (uint32_t)img.size(); ctx->udp_bits = bu;
+    img.insert(img.end(), hu.begin(), hu.end());
+  } else {
+    ctx->use_pages = 1;
+    std::vector<uint16_t> blob = encode_tables(eth.data(), proto.data(), tcp.data(), udp.data());
+    HIP_TRY(hipMalloc(&ctx->d_pages, blob.size() * sizeof(uint16_t)));
+    HIP_TRY(hipMemcpy(ctx->d_pages, blob.data(), blob.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
   }
-  if (!ctx->d_tables) {
-    HIP_TRY(hipMalloc(&ctx->d_tables, blob.size() * sizeof(uint16_t)));
-    ctx->tables_words = blob.size();
-  }
-  HIP_TRY(hipMemcpy(ctx->d_tables, blob.data(), blob.size() * sizeof(uint16_t),
-                    hipMemcpyHostToDevice));
+  ctx->image_words = (uint32_t)img.size();
+  HIP_TRY(hipMalloc(&ctx->d_image, img.size() * sizeof(uint32_t)));
+  HIP_TRY(hipMemcpy(ctx->d_image, img.data(), img.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
   return GPD_OK;
 }
 
@@ -207,7 +261,8 @@ int gpd_ctx_destroy(gpd_ctx *ctx) {
   if (!ctx) return GPD_OK;
   (void)hipSetDevice(ctx->device);
   free_slots(ctx);
-  if (ctx->d_tables) (void)hipFree(ctx->d_tables);
+  if (ctx->d_image) (void)hipFree(ctx->d_image);
+  if (ctx->d_pages) (void)hipFree(ctx->d_pages);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   delete ctx;
@@ -263,7 +318,15 @@ static int launch(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, hipS
   P.tp_hash = out->tp_hash;
   P.csum = out->csum;
   P.ext = out->ext;
-  P.tables = ctx->d_tables;
+  P.image = ctx->d_image;
+  P.pages = ctx->d_pages;
+  P.image_words = ctx->image_words;
+  P.use_pages = ctx->use_pages;
+  P.eth_base = ctx->eth_base; P.tcp_base = ctx->tcp_base; P.udp_base = ctx->udp_base;
+  P.eth_bits = ctx->eth_bits; P.tcp_bits = ctx->tcp_bits; P.udp_bits = ctx->udp_bits;
+  // LDS window per buffer: the smallest of 4/8 KiB that holds a typical 64-packet tile
+  const uint64_t mean_slot = (in->data_len + in->n - 1) / in->n;
+  P.stage = mean_slot * 64 <= 4096 ? 4096u : 8192u;
   P.first = ctx->first;
   P.decoders = ctx->decoders;
   P.options = ctx->options;
