@@ -83,6 +83,8 @@ def main():
     ap.add_argument("--packets", type=int, default=0, help="override packets per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--ablate", default="", help="diagnostics only: 'nocsum', 'nohash' or both "
+                    "(comma separated); never used for the reported metric")
     args = ap.parse_args()
 
     import torch
@@ -109,6 +111,30 @@ def main():
                                       P.IPv6(), P.IPv6ExtensionSkipper(), P.TCP(), P.UDP(),
                                       P.VXLAN(), P.Payload(), P.Fragment(), device=local)
     stream = torch.cuda.current_stream(local)
+    if "nocsum" in args.ablate:
+        parser.ComputeChecksums = False
+    if "nohash" in args.ablate:
+        parser.ComputeFlowHashes = False
+    if "nodecode" in args.ablate:
+        parser._diag_options = 1 << 31  # kernel streams the windows and skips decoding
+    if "nowait" in args.ablate:
+        parser._diag_options = 1 << 30  # kernel skips the per-tile DMA wait (wrong results)
+    if "copy" in args.ablate:  # reference: device-to-device copy of the packet bytes
+        src = dev_batch.data
+        dst = torch.empty_like(src)
+        for _ in range(3):
+            dst.copy_(src)
+        torch.cuda.synchronize(local)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(20):
+            dst.copy_(src)
+        e1.record(stream)
+        torch.cuda.synchronize(local)
+        ms = e0.elapsed_time(e1) / 20
+        print(json.dumps({"diag": "torch copy", "bytes": src.numel(), "ms": ms,
+                          "GBps_read_plus_write": 2 * src.numel() / ms / 1e6}), flush=True)
+        return
 
     for _ in range(args.warmup):
         parser.decode_device(dev_batch, dev_res, stream)
@@ -169,7 +195,10 @@ def main():
                      "total_frac_with_results": round((read_bytes + write_bytes * n) /
                                                       (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if args.ablate:
+        out["ablation"] = args.ablate
+        out["metric"] = "DIAGNOSTIC ablation (not the metric): " + out["metric"]
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.ablate:
         out["cpu_baseline"] = cpu_baseline(batch, args.cpu_budget)
     if rank == 0:
         print(json.dumps(out), flush=True)

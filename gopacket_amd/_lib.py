@@ -9,7 +9,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgpd.so")
+LIB_PATH = os.environ.get("GPD_LIB_PATH") or os.path.join(_HERE, "libgpd.so")  # override: A/B only
 
 GPD_ABI_VERSION = 1
 GPD_OK = 0

@@ -13,11 +13,13 @@ namespace gpd {
 //
 // (a) HASH (default, copied into LDS by every workgroup): the tables are sparse (the
 //     reference defaults hold 18 + 11 + 16 nonzero 16-bit entries), so each 64K table
-//     is an open-addressed hash of its nonzero entries, u32 slots {key:16 | value:16}
-//     (value 0 never stored => an empty slot ends the probe).  Layout in u32 words:
+//     is an open-addressed, linearly probed hash of its nonzero entries with u32 slots
+//     {key << 16 | LayerType << 8 | LUT entry of that LayerType} (so one LDS read yields
+//     both the next LayerType and its decoder; needs every mapped LayerType < 256).
+//     Layout in u32 words:
 //       [0,32)                     type LUT: byte t = decoder id | code << 4 for t < 128
 //                                  (decoder id 15 = not registered)
-//       [32,160)                   ipproto -> LayerType (u16 pairs)
+//       [32,288)                   ipproto -> LayerType | LUT entry << 16
 //       [eth_base, +2^eth_bits)    ethertype hash
 //       [tcp_base, +2^tcp_bits)    tcp port hash
 //       [udp_base, +2^udp_bits)    udp port hash
@@ -26,7 +28,7 @@ namespace gpd {
 //     [256,512) eth dir, [512,768) tcp dir, [768,1024) udp dir, then 256-entry pages
 //     (page 0 = zeros).
 constexpr uint32_t kHashLutWords = 32;
-constexpr uint32_t kHashProtoWords = 128;
+constexpr uint32_t kHashProtoWords = 256;
 constexpr uint32_t kHashMaxWords = 4096;  // 16 KB cap for the LDS image
 constexpr uint32_t kTabIpProto = 0;
 constexpr uint32_t kTabEthDir = 256;

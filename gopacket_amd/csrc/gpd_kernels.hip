@@ -32,12 +32,14 @@
 // DESIGN.md §Semantics defines every output word.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "gpd_internal.h"
 
 namespace gpd {
 
-constexpr int kWaves = 4;            // waves per workgroup
-constexpr int kBlock = 64 * kWaves;  // threads per workgroup
+constexpr uint32_t kDiagSkipDecode = 1u << 31;  // internal diagnostic option (bench --ablate nodecode)
+constexpr uint32_t kDiagNoWait = 1u << 30;      // internal diagnostic: skip the per-tile DMA wait
 
 extern __shared__ __attribute__((aligned(16))) uint8_t g_lds[];
 
@@ -105,47 +107,54 @@ enum Dec : uint32_t {
   D_ETH, D_DOT1Q, D_IP4, D_IP6, D_IP6EXT, D_TCP, D_UDP, D_VXLAN, D_PAYLOAD, D_FRAG, D_NONE = 15
 };
 
+struct TE {        // a dispatch-table result
+  uint32_t lt;     // LayerType (0: none / unknown)
+  uint32_t ent;    // its type-LUT entry: decoder id (15 = not registered) | layer code << 4
+};
+
 template <bool PAGES>
 struct Tab {
   const uint16_t *pages;
   uint32_t eth_base, tcp_base, udp_base, eth_bits, tcp_bits, udp_bits;
 
-  // type LUT: decoder id (15 = none) | layer code << 4  (registered set applied by the host)
+  // type LUT (registered set applied by the host)
   __device__ __forceinline__ uint32_t lut(uint32_t t) const { return t < 128 ? g_lds[t] : 0xFFu; }
-  __device__ __forceinline__ uint32_t proto(uint32_t p) const {  // enums_generated.go:151-153
-    return *reinterpret_cast<const uint16_t *>(g_lds + 128 + 2 * (p & 0xFFu));
+  __device__ __forceinline__ TE proto(uint32_t p) const {  // enums_generated.go:151-153
+    const uint32_t v = lds_u32(4 * (kHashLutWords + (p & 0xFFu)));
+    return TE{v & 0xFFFFu, v >> 16};
   }
-  __device__ __forceinline__ uint32_t hash(uint32_t base, uint32_t bits, uint32_t key) const {
+  __device__ __forceinline__ TE hash(uint32_t base, uint32_t bits, uint32_t key) const {
     const uint32_t mask = (1u << bits) - 1;
     uint32_t h = key_hash(key, bits);
-    for (;;) {
-      uint32_t v = lds_u32(4 * (base + h));
-      if ((v & 0xFFFFu) == 0) return 0;
-      if ((v >> 16) == key) return v & 0xFFFFu;
+    for (;;) {  // linear probing; an empty slot ends it (the host bounds probes at 8)
+      const uint32_t v = lds_u32(4 * (base + h));
+      if (v == 0) return TE{0u, 0xFFu};
+      if ((v >> 16) == key) return TE{(v >> 8) & 0xFFu, v & 0xFFu};
       h = (h + 1) & mask;
     }
   }
-  __device__ __forceinline__ uint32_t page(uint32_t dir, uint32_t key) const {
-    uint32_t pg = pages[dir + (key >> 8)];
-    return pages[kTabPages + pg * 256u + (key & 0xFFu)];
+  __device__ __forceinline__ TE page(uint32_t dir, uint32_t key) const {
+    const uint32_t pg = pages[dir + (key >> 8)];
+    const uint32_t lt = pages[kTabPages + pg * 256u + (key & 0xFFu)];
+    return TE{lt, lut(lt)};
   }
-  __device__ __forceinline__ uint32_t eth(uint32_t et) const {  // enums_generated.go:77-79
+  __device__ __forceinline__ TE eth(uint32_t et) const {  // enums_generated.go:77-79
     return PAGES ? page(kTabEthDir, et) : hash(eth_base, eth_bits, et);
   }
-  __device__ __forceinline__ uint32_t tcp(uint32_t port) const {  // ports.go:54-60 (raw)
+  __device__ __forceinline__ TE tcp(uint32_t port) const {  // ports.go:54-60 (raw)
     return PAGES ? page(kTabTcpDir, port) : hash(tcp_base, tcp_bits, port);
   }
-  __device__ __forceinline__ uint32_t udp(uint32_t port) const {  // ports.go:97-103 (raw)
+  __device__ __forceinline__ TE udp(uint32_t port) const {  // ports.go:97-103 (raw)
     return PAGES ? page(kTabUdpDir, port) : hash(udp_base, udp_bits, port);
   }
 };
 
 // TCP/UDP NextLayerType: dst port table, else src port table; 0 => Payload
 // (tcp.go:308-314, udp.go:105-110).  Both lookups are issued together.
-__device__ __forceinline__ uint32_t ports_next(uint32_t ld, uint32_t ls) {
-  ld = ld ? ld : (uint32_t)GPD_LT_PAYLOAD;
-  ls = ls ? ls : (uint32_t)GPD_LT_PAYLOAD;
-  return ld != GPD_LT_PAYLOAD ? ld : ls;
+__device__ __forceinline__ TE ports_next(TE d, TE s, uint32_t payload_ent) {
+  d = d.lt ? d : TE{(uint32_t)GPD_LT_PAYLOAD, payload_ent};
+  s = s.lt ? s : TE{(uint32_t)GPD_LT_PAYLOAD, payload_ent};
+  return d.lt != GPD_LT_PAYLOAD ? d : s;
 }
 
 // ---------------------------------------------------------------- checksums / hashes
@@ -249,7 +258,7 @@ __device__ __forceinline__ Out decode_packet(const S &s, uint32_t caplen, const 
             else p_len = et;
             et = 0;  // EthernetTypeLLC
           }
-          next = T.eth(et);
+          next = T.eth(et).lt;
           break;
         }
         case D_DOT1Q: {  // dot1q.go:29-40
@@ -257,7 +266,7 @@ __device__ __forceinline__ Out decode_packet(const S &s, uint32_t caplen, const 
           uint32_t w[1];
           load_words(s, off, w);
           c_len = 4; p_off = off + 4; p_len = len - 4;
-          next = T.eth(be16_at(w, 2));
+          next = T.eth(be16_at(w, 2)).lt;
           break;
         }
         case D_IP4: {  // ip4.go:188-286
@@ -291,7 +300,7 @@ __device__ __forceinline__ Out decode_packet(const S &s, uint32_t caplen, const 
             if (ol <= 2) GPD_FAIL(GPD_E_IP4_OPT_LE2, t, ol);
             q += ol;
           }
-          next = ((ff >> 13) & 1u) || (ff & 0x1FFFu) ? (uint32_t)GPD_LT_FRAGMENT : T.proto(proto);
+          next = ((ff >> 13) & 1u) || (ff & 0x1FFFu) ? (uint32_t)GPD_LT_FRAGMENT : T.proto(proto).lt;
           break;
         }
         case D_IP6: {  // ip6.go:221-291
@@ -334,7 +343,7 @@ __device__ __forceinline__ Out decode_packet(const S &s, uint32_t caplen, const 
             if (jumbo && length == 0) {
               if (jumbo_len > p_len) truncated = 1;
               else p_len = jumbo_len;  // payload still starts at the HBH header (ip6.go:255)
-              next = T.proto(use_nh);
+              next = T.proto(use_nh).lt;
               break;
             } else if (jumbo) {
               GPD_FAIL(GPD_E_IP6_JUMBO_AND_LEN, 0, 0);
@@ -347,7 +356,7 @@ __device__ __forceinline__ Out decode_packet(const S &s, uint32_t caplen, const 
           if (length == 0) GPD_FAIL(GPD_E_IP6_LEN0_NOT_HBH, nh, 0);
           if (length > p_len) truncated = 1;
           else p_len = length;
-          next = T.proto(use_nh);
+          next = T.proto(use_nh).lt;
           break;
         }
         case D_IP6EXT: {  // ip6.go:418-432,443-461
@@ -357,14 +366,14 @@ __device__ __forceinline__ Out decode_packet(const S &s, uint32_t caplen, const 
           uint32_t actual = byte_at(w, 1) * 8u + 8u;
           if (len < actual) GPD_FAIL(GPD_E_IP6EXT_LT_SPEC, len, actual);
           c_len = actual; p_off = off + actual; p_len = len - actual;
-          next = T.proto(byte_at(w, 0));
+          next = T.proto(byte_at(w, 0)).lt;
           break;
         }
         case D_TCP: {  // tcp.go:229-314
           if (len < 20) { truncated = 1; GPD_FAIL(GPD_E_TCP_TOO_SHORT, len, 0); }
           uint32_t w[4];
           load_words(s, off, w);  // bytes 0..15: ports .. flags
-          const uint32_t ld = T.tcp(be16_at(w, 2)), ls = T.tcp(be16_at(w, 0));
+          const TE ld = T.tcp(be16_at(w, 2)), ls = T.tcp(be16_at(w, 0));
           uint32_t doff = byte_at(w, 12) >> 4;
           if (doff < 5) GPD_FAIL(GPD_E_TCP_DOFF_LT5, doff, 0);
           uint32_t ds = doff * 4;
@@ -382,14 +391,14 @@ __device__ __forceinline__ Out decode_packet(const S &s, uint32_t caplen, const 
             }
             q += ol;
           }
-          next = ports_next(ld, ls);
+          next = ports_next(ld, ls, 0).lt;
           break;
         }
         case D_UDP: {  // udp.go:30-56,105-110
           if (len < 8) { truncated = 1; GPD_FAIL(GPD_E_UDP_TOO_SHORT, len, 0); }
           uint32_t w[2];
           load_words(s, off, w);
-          const uint32_t ld = T.udp(be16_at(w, 2)), ls = T.udp(be16_at(w, 0));
+          const TE ld = T.udp(be16_at(w, 2)), ls = T.udp(be16_at(w, 0));
           uint32_t length = be16_at(w, 4);
           c_len = 8; p_off = off + 8;
           if (length >= 8) {
@@ -401,7 +410,7 @@ __device__ __forceinline__ Out decode_packet(const S &s, uint32_t caplen, const 
           } else {
             GPD_FAIL(GPD_E_UDP_LEN_TOO_SMALL, length, 0);
           }
-          next = ports_next(ld, ls);
+          next = ports_next(ld, ls, 0).lt;
           break;
         }
         case D_VXLAN: {  // vxlan.go:53-78
@@ -572,13 +581,21 @@ struct Fast {
   uint64_t nhash;
 };
 
+struct FastCtx {        // wave-uniform facts about the registered set
+  uint32_t eth_code;    // layer code of Ethernet
+  uint32_t dq_code;     // layer code of Dot1Q
+  bool dq;              // Dot1Q registered
+  uint32_t pl_ent;      // LUT entry of Payload
+};
+
 // Transport at compile-time offset T4 with `tl` bytes available (the network payload).
 template <int T4, bool PAGES>
 __device__ __forceinline__ bool fast_tp(const LdsSrc &s, const uint32_t (&h)[20], uint32_t tl,
                                         uint32_t dec, uint32_t code, const Tab<PAGES> &T,
-                                        Fast &f, uint32_t &seg_sum, uint32_t &seg_len,
-                                        uint64_t &thash) {
-  uint32_t next, plen;
+                                        const FastCtx &F, Fast &f, uint32_t &seg_sum,
+                                        uint32_t &seg_len, uint64_t &thash) {
+  TE next;
+  uint32_t plen;
   if (dec == D_TCP) {  // tcp.go:229-314
     if (tl < 20) return false;
     const uint32_t doff = fbyte<T4 + 12>(h) >> 4;
@@ -596,7 +613,7 @@ __device__ __forceinline__ bool fast_tp(const LdsSrc &s, const uint32_t (&h)[20]
       }
       q += ol;
     }
-    next = ports_next(T.tcp(fbe16<T4 + 2>(h)), T.tcp(fbe16<T4>(h)));
+    next = ports_next(T.tcp(fbe16<T4 + 2>(h)), T.tcp(fbe16<T4>(h)), F.pl_ent);
     plen = tl - ds;
     seg_len = tl;
   } else {  // UDP, udp.go:30-56
@@ -611,7 +628,7 @@ __device__ __forceinline__ bool fast_tp(const LdsSrc &s, const uint32_t (&h)[20]
     } else {
       return false;
     }
-    next = ports_next(T.udp(fbe16<T4 + 2>(h)), T.udp(fbe16<T4>(h)));
+    next = ports_next(T.udp(fbe16<T4 + 2>(h)), T.udp(fbe16<T4>(h)), F.pl_ent);
     plen = hl - 8;
     seg_len = hl;
   }
@@ -622,10 +639,9 @@ __device__ __forceinline__ bool fast_tp(const LdsSrc &s, const uint32_t (&h)[20]
   f.codes |= (uint64_t)code << (16 + 4 * f.ncount);
   f.ncount++;
   if (plen == 0) return true;
-  const uint32_t ent = T.lut(next);
-  if ((ent & 15u) == D_NONE) { f.stop = next; return true; }
-  if ((ent & 15u) != D_PAYLOAD) return false;  // e.g. VXLAN, a registered app layer
-  f.codes |= (uint64_t)(ent >> 4) << (16 + 4 * f.ncount);  // Payload consumes the rest
+  if ((next.ent & 15u) == D_NONE) { f.stop = next.lt; return true; }
+  if ((next.ent & 15u) != D_PAYLOAD) return false;  // e.g. VXLAN, a registered app layer
+  f.codes |= (uint64_t)(next.ent >> 4) << (16 + 4 * f.ncount);  // Payload consumes the rest
   f.ncount++;
   return true;
 }
@@ -633,12 +649,13 @@ __device__ __forceinline__ bool fast_tp(const LdsSrc &s, const uint32_t (&h)[20]
 // Network layer at compile-time offset L3; `typ` is the LayerType Ethernet/Dot1Q chose.
 template <int L3, bool PAGES>
 __device__ __forceinline__ bool fast_l3(const LdsSrc &s, const uint32_t (&h)[20], uint32_t len,
-                                        uint32_t typ, const Tab<PAGES> &T, Fast &f,
+                                        TE typ, const Tab<PAGES> &T, const FastCtx &F, Fast &f,
                                         uint32_t &seg_sum, uint32_t &seg_len, uint64_t &thash) {
-  const uint32_t ent = T.lut(typ);
+  const uint32_t ent = typ.ent;
   const uint32_t dec = ent & 15u;
   const uint32_t dl = len - L3;
-  uint32_t next, plen;
+  TE next;
+  uint32_t plen;
   if (dec == D_IP4) {  // ip4.go:188-286
     if (dl < 20) return false;
     const uint32_t w0 = word_at<L3>(h), w1 = word_at<L3 + 4>(h), w2 = word_at<L3 + 8>(h);
@@ -708,20 +725,19 @@ __device__ __forceinline__ bool fast_l3(const LdsSrc &s, const uint32_t (&h)[20]
   f.codes |= (uint64_t)(ent >> 4) << (16 + 4 * f.ncount);
   f.ncount++;
   if (plen == 0) return true;
-  const uint32_t e2 = T.lut(next);
-  const uint32_t d2 = e2 & 15u;
-  if (d2 == D_NONE) { f.stop = next; return true; }
+  const uint32_t d2 = next.ent & 15u;
+  if (d2 == D_NONE) { f.stop = next.lt; return true; }
   if (d2 != D_TCP && d2 != D_UDP) return false;
   if (dec == D_IP4)
-    return fast_tp<L3 + 20>(s, h, plen, d2, e2 >> 4, T, f, seg_sum, seg_len, thash);
+    return fast_tp<L3 + 20>(s, h, plen, d2, next.ent >> 4, T, F, f, seg_sum, seg_len, thash);
   if constexpr (L3 <= 18)
-    return fast_tp<L3 + 40>(s, h, plen, d2, e2 >> 4, T, f, seg_sum, seg_len, thash);
+    return fast_tp<L3 + 40>(s, h, plen, d2, next.ent >> 4, T, F, f, seg_sum, seg_len, thash);
   return false;
 }
 
 template <bool PAGES>
 __device__ __forceinline__ bool fast_decode(const LdsSrc &s, uint32_t len, const Tab<PAGES> &T,
-                                            uint32_t options, Out &o) {
+                                            const FastCtx &F, uint32_t options, Out &o) {
   if (len < 14) return false;
   uint32_t h[20];
 #pragma unroll
@@ -730,35 +746,33 @@ __device__ __forceinline__ bool fast_decode(const LdsSrc &s, uint32_t len, const
     h[4 * k] = v.x; h[4 * k + 1] = v.y; h[4 * k + 2] = v.z; h[4 * k + 3] = v.w;
   }
   Fast f{0, 1, 0, 0, 0, 0, 0, 0, 0};
-  const uint32_t eth_ent = T.lut(GPD_LT_ETHERNET);
-  f.codes = (uint64_t)(eth_ent >> 4) << 16;  // Ethernet, ethernet.go:41-62
+  f.codes = (uint64_t)F.eth_code << 16;     // Ethernet, ethernet.go:41-62
   const uint32_t et = fbe16<12>(h);
   if (et < 0x0600u) return false;            // 802.3 length framing: generic path
-  uint32_t typ = T.eth(et);
+  TE typ = T.eth(et);
   uint32_t seg_sum = 0, seg_len = 0;
   uint64_t thash = 0;
   bool ok;
-  const uint32_t dq = T.lut(GPD_LT_DOT1Q);
-  if ((typ == GPD_LT_DOT1Q) && (dq & 15u) == D_DOT1Q) {  // dot1q.go:29-50
+  if (typ.lt == GPD_LT_DOT1Q && F.dq) {  // dot1q.go:29-50
     if (len < 18) return false;
-    f.codes |= (uint64_t)(dq >> 4) << 20;
+    f.codes |= (uint64_t)F.dq_code << 20;
     f.ncount = 2;
     typ = T.eth(fbe16<16>(h));
-    if (typ == GPD_LT_DOT1Q) {
+    if (typ.lt == GPD_LT_DOT1Q) {
       if (len < 22) return false;
-      f.codes |= (uint64_t)(dq >> 4) << 24;
+      f.codes |= (uint64_t)F.dq_code << 24;
       f.ncount = 3;
       typ = T.eth(fbe16<20>(h));
-      if (typ == GPD_LT_DOT1Q) return false;
+      if (typ.lt == GPD_LT_DOT1Q) return false;
       if (len == 22) return false;  // empty Dot1Q payload: generic path ends the loop there
-      ok = fast_l3<22>(s, h, len, typ, T, f, seg_sum, seg_len, thash);
+      ok = fast_l3<22>(s, h, len, typ, T, F, f, seg_sum, seg_len, thash);
     } else {
       if (len == 18) return false;
-      ok = fast_l3<18>(s, h, len, typ, T, f, seg_sum, seg_len, thash);
+      ok = fast_l3<18>(s, h, len, typ, T, F, f, seg_sum, seg_len, thash);
     }
   } else {
     if (len == 14) return false;
-    ok = fast_l3<14>(s, h, len, typ, T, f, seg_sum, seg_len, thash);
+    ok = fast_l3<14>(s, h, len, typ, T, F, f, seg_sum, seg_len, thash);
   }
   if (!ok) return false;
   // status / layers / hashes / checksums exactly as decode_packet composes them
@@ -854,8 +868,10 @@ __device__ __forceinline__ void issue_window(const uint8_t *data, const Window &
 }
 
 // ---------------------------------------------------------------- kernel
-template <int STAGE, bool EXT, bool PAGES>
-__global__ __launch_bounds__(kBlock) void decode_kernel(KParams P) {
+// WAVES waves per workgroup; MINW = waves per SIMD the register allocation must allow.
+template <int STAGE, bool EXT, bool PAGES, int WAVES, int MINW>
+__global__ __launch_bounds__(64 * WAVES, MINW) void decode_kernel(KParams P) {
+  constexpr int kWaves = WAVES, kBlock = 64 * WAVES;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = threadIdx.x >> 6;
   // stage the dispatch-table image (LUT, ipproto, hashes) into LDS
@@ -869,7 +885,9 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(KParams P) {
   const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
   const uint32_t fits = (uint32_t)STAGE - 15u;  // a packet of <= fits bytes always fits a window
   // the fast path assumes Ethernet first (DecodingLayerParser built with LayerTypeEthernet)
-  const bool fast_ok = P.first == GPD_LT_ETHERNET && (T.lut(GPD_LT_ETHERNET) & 15u) == D_ETH;
+  const bool fast_ok = !PAGES && P.first == GPD_LT_ETHERNET && (T.lut(GPD_LT_ETHERNET) & 15u) == D_ETH;
+  const FastCtx F{T.lut(GPD_LT_ETHERNET) >> 4, T.lut(GPD_LT_DOT1Q) >> 4,
+                  (T.lut(GPD_LT_DOT1Q) & 15u) == D_DOT1Q, T.lut(GPD_LT_PAYLOAD)};
 
   uint64_t t = (uint64_t)blockIdx.x * kWaves + wave;
   if (t >= ntiles) return;
@@ -887,7 +905,7 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(KParams P) {
 
   for (;;) {
     // this tile's window and the next tile's descriptors were issued one decode ago
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!(P.options & kDiagNoWait)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const bool has_next = tn < ntiles;
     Window Wn{0, 0};
     if (has_next) {  // next tile's first window streams in while this tile decodes
@@ -919,10 +937,14 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(KParams P) {
       }
       firstw = false;
       const bool in = pending && off >= W.base && (uint64_t)off + len <= (uint64_t)W.base + STAGE;
-      if (in) {
+      if (in && (P.options & kDiagSkipDecode)) {  // diagnostics: data movement only
+        o = Out{g_lds[buf + ((off - W.base) & ~15u)], 0, 0, 0, 0};
+        store_out(P, i, o);
+        pending = false;
+      } else if (in) {
         const LdsSrc src{buf, off - W.base};
         bool done = false;
-        if (!EXT && fast_ok && (src.pos & 15u) == 0) done = fast_decode<PAGES>(src, len, T, P.options, o);
+        if (!EXT && fast_ok && (src.pos & 15u) == 0) done = fast_decode<PAGES>(src, len, T, F, P.options, o);
         if (!done) o = decode_packet<EXT>(src, len, T, P.first, P.options, ext);
         store_out(P, i, o);
         pending = false;
@@ -945,27 +967,46 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(KParams P) {
   }
 }
 
-template <int STAGE, bool EXT, bool PAGES>
+template <int STAGE, bool EXT, bool PAGES, int WAVES, int MINW>
 static hipError_t launch_t(const KParams &P, hipStream_t stream, int num_cus) {
   const uint64_t ntiles = (P.n + 63) / 64;
   const size_t img = (P.image_words * 4u + 15u) & ~15u;
-  const size_t lds = img + (size_t)STAGE * 2 * kWaves + 320;  // slack: rotated reads past a window end
+  const size_t lds = img + (size_t)STAGE * 2 * WAVES + 320;  // slack: rotated reads past a window end
   const uint64_t per_cu = (160u * 1024u) / lds;               // resident workgroups per CU (LDS)
-  uint64_t blocks = (ntiles + kWaves - 1) / kWaves;
+  uint64_t blocks = (ntiles + WAVES - 1) / WAVES;
   const uint64_t cap = (uint64_t)num_cus * (per_cu ? per_cu : 1) * 4;  // a few tiles per wave
   if (blocks > cap) blocks = cap;
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL((decode_kernel<STAGE, EXT, PAGES>), dim3((unsigned)blocks), dim3(kBlock), lds,
-                     stream, P);
+  hipLaunchKernelGGL((decode_kernel<STAGE, EXT, PAGES, WAVES, MINW>), dim3((unsigned)blocks),
+                     dim3(64 * WAVES), lds, stream, P);
   return hipGetLastError();
+}
+
+// Geometry variants (diagnostic selector GPD_GEOM: 0 = 4 waves/WG, 1 = 2 waves/WG with a
+// 5-waves-per-SIMD register budget, 2 = 4 waves/WG with that budget, 3 = 2 waves/WG).
+static int geom() {
+  static int g = -1;
+  if (g < 0) {
+    const char *e = getenv("GPD_GEOM");
+    g = e ? atoi(e) : 0;
+  }
+  return g;
 }
 
 template <bool EXT, bool PAGES>
 static hipError_t launch_s(const KParams &P, hipStream_t stream, int num_cus) {
+  const int g = geom();
   switch (P.stage) {
-    case 4096: return launch_t<4096, EXT, PAGES>(P, stream, num_cus);
-    case 8192: return launch_t<8192, EXT, PAGES>(P, stream, num_cus);
-    default: return launch_t<16384, EXT, PAGES>(P, stream, num_cus);
+    case 4096:
+      if (g == 1) return launch_t<4096, EXT, PAGES, 2, 5>(P, stream, num_cus);
+      if (g == 2) return launch_t<4096, EXT, PAGES, 4, 5>(P, stream, num_cus);
+      if (g == 3) return launch_t<4096, EXT, PAGES, 2, 1>(P, stream, num_cus);
+      return launch_t<4096, EXT, PAGES, 4, 1>(P, stream, num_cus);
+    default:
+      if (g == 1) return launch_t<8192, EXT, PAGES, 2, 5>(P, stream, num_cus);
+      if (g == 2) return launch_t<8192, EXT, PAGES, 4, 5>(P, stream, num_cus);
+      if (g == 3) return launch_t<8192, EXT, PAGES, 2, 1>(P, stream, num_cus);
+      return launch_t<8192, EXT, PAGES, 4, 1>(P, stream, num_cus);
   }
 }
 
@@ -977,3 +1018,18 @@ hipError_t launch_decode(const KParams &P, hipStream_t stream, int num_cus) {
 }
 
 }  // namespace gpd
+
+#ifdef GPD_ISA_PROBE
+// Instruction-count probe (not built into libgpd.so): the fast path alone on one packet.
+namespace gpd {
+__global__ void probe_fast(KParams P) {
+  const uint32_t pos = P.offset[threadIdx.x], len = P.caplen[threadIdx.x];
+  const Tab<false> T{P.pages, P.eth_base, P.tcp_base, P.udp_base, P.eth_bits, P.tcp_bits, P.udp_bits};
+  Out o{};
+  const FastCtx F{1, 2, true, 0xC8};
+  const bool ok = fast_decode<false>(LdsSrc{0, pos}, len, T, F, P.options, o);
+  const uint32_t i = threadIdx.x;
+  if (ok) store_out(P, i, o);
+}
+}  // namespace gpd
+#endif

@@ -100,13 +100,17 @@ void type_lut(uint32_t decoders, uint8_t lut[128]) {
     if (decoders & (1u << e.dec)) lut[e.lt] = (uint8_t)(e.dec | (e.code << 4));
 }
 
-// Open-addressed hash of the nonzero entries of a 64K table; returns log2(slots) or 0 if it
-// would not fit `max_slots` with every probe sequence <= 8.
-uint32_t build_hash(const uint16_t *t, uint32_t max_slots, std::vector<uint32_t> &slots) {
+// Open-addressed (linear probing) hash of the nonzero entries of a 64K table, u32 slots
+// {key << 16 | LayerType << 8 | lut[LayerType]}; usable when every LayerType is < 256 and
+// no probe sequence exceeds 8.  Returns log2(slots), or 0 when the table does not qualify.
+uint32_t build_hash(const uint16_t *t, const uint8_t lut[128], uint32_t max_words,
+                    std::vector<uint32_t> &slots) {
   std::vector<uint32_t> keys;
-  for (uint32_t k = 0; k < 65536; k++)
+  for (uint32_t k = 0; k < 65536; k++) {
+    if (t[k] >= 256) return 0;
     if (t[k]) keys.push_back(k);
-  for (uint32_t bits = 4; (1u << bits) <= max_slots && bits <= 16; bits++) {
+  }
+  for (uint32_t bits = 4; bits <= 16 && (1u << bits) <= max_words; bits++) {
     const uint32_t n = 1u << bits, mask = n - 1;
     if (keys.size() * 2 > n) continue;
     slots.assign(n, 0);
@@ -115,7 +119,7 @@ uint32_t build_hash(const uint16_t *t, uint32_t max_slots, std::vector<uint32_t>
       uint32_t h = gpd::key_hash(k, bits), probe = 0;
       while (slots[h]) { h = (h + 1) & mask; probe++; }
       if (probe >= 8) { ok = false; break; }
-      slots[h] = (k << 16) | t[k];
+      slots[h] = (k << 16) | ((uint32_t)t[k] << 8) | (t[k] < 128 ? lut[t[k]] : 0xFFu);
     }
     if (ok) return bits;
   }
@@ -174,15 +178,19 @@ int gpd_ctx_reload_tables(gpd_ctx *ctx, const gpd_config *cfg) {
   if (cfg->ipproto) std::memcpy(proto.data(), cfg->ipproto, 256 * 2);
   if (cfg->tcp_port) std::memcpy(tcp.data(), cfg->tcp_port, 65536 * 2);
   if (cfg->udp_port) std::memcpy(udp.data(), cfg->udp_port, 65536 * 2);
-  // LDS image: LUT (32 words) + ipproto (128 words) + the three hashes
+  // LDS image: LUT (32 words) + ipproto with LUT entries (256 words) + the three hashes
   std::vector<uint32_t> img(gpd::kHashLutWords + gpd::kHashProtoWords, 0);
-  type_lut(ctx->decoders, reinterpret_cast<uint8_t *>(img.data()));
-  std::memcpy(img.data() + gpd::kHashLutWords, proto.data(), 256 * sizeof(uint16_t));
+  uint8_t *lut = reinterpret_cast<uint8_t *>(img.data());
+  type_lut(ctx->decoders, lut);
+  for (uint32_t p = 0; p < 256; p++) {
+    const uint32_t lt = proto[p];
+    img[gpd::kHashLutWords + p] = lt | ((lt < 128 ? lut[lt] : 0xFFu) << 16);
+  }
   std::vector<uint32_t> he, ht, hu;
   const uint32_t room = gpd::kHashMaxWords - (uint32_t)img.size();
-  uint32_t be = build_hash(eth.data(), room / 2, he);
-  uint32_t bt = be ? build_hash(tcp.data(), room / 4, ht) : 0;
-  uint32_t bu = bt ? build_hash(udp.data(), room / 4, hu) : 0;
+  uint32_t be = build_hash(eth.data(), lut, room / 2, he);  // 0 => PAGES mode
+  uint32_t bt = be ? build_hash(tcp.data(), lut, room / 4, ht) : 0;
+  uint32_t bu = bt ? build_hash(udp.data(), lut, room / 4, hu) : 0;
   HIP_TRY(hipSetDevice(ctx->device));
   if (ctx->d_image) { HIP_TRY(hipFree(ctx->d_image)); ctx->d_image = nullptr; }
   if (ctx->d_pages) { HIP_TRY(hipFree(ctx->d_pages)); ctx->d_pages = nullptr; }

@@ -211,6 +211,7 @@ class DecodingLayerParser:
         o |= OPT_IGNORE_PANIC if self.IgnorePanic else 0
         o |= 0 if self.ComputeChecksums else OPT_NO_CHECKSUMS
         o |= 0 if self.ComputeFlowHashes else OPT_NO_FLOW_HASH
+        o |= getattr(self, "_diag_options", 0)
         return o
 
     def ctx(self) -> _Ctx:
