@@ -13,16 +13,18 @@ namespace gpd {
 //
 // (a) HASH (default, copied into LDS by every workgroup): the tables are sparse (the
 //     reference defaults hold 18 + 11 + 16 nonzero 16-bit entries), so each 64K table
-//     is an open-addressed, linearly probed hash of its nonzero entries with u32 slots
-//     {key << 16 | LayerType << 8 | LUT entry of that LayerType} (so one LDS read yields
-//     both the next LayerType and its decoder; needs every mapped LayerType < 256).
+//     is a two-way bucketed hash of its nonzero entries: 2^bits buckets of two u32 slots
+//     {key << 16 | LayerType << 8 | LUT entry of that LayerType}, with a per-table
+//     multiplier chosen by the host so that no bucket overflows.  One ds_read_b64 yields
+//     both candidates, and the matching slot gives the next LayerType and its decoder
+//     (needs every mapped LayerType < 256).
 //     Layout in u32 words:
 //       [0,32)                     type LUT: byte t = decoder id | code << 4 for t < 128
 //                                  (decoder id 15 = not registered)
 //       [32,288)                   ipproto -> LayerType | LUT entry << 16
-//       [eth_base, +2^eth_bits)    ethertype hash
-//       [tcp_base, +2^tcp_bits)    tcp port hash
-//       [udp_base, +2^udp_bits)    udp port hash
+//       [eth_base, +2^(eth_bits+1))  ethertype hash (8-byte aligned)
+//       [tcp_base, +2^(tcp_bits+1))  tcp port hash
+//       [udp_base, +2^(udp_bits+1))  udp port hash
 // (b) PAGES (fallback when a table is too dense for the LDS budget): the image holds only
 //     the LUT and ipproto; the 64K tables are two-level pages in global memory, u16 words:
 //     [256,512) eth dir, [512,768) tcp dir, [768,1024) udp dir, then 256-entry pages
@@ -53,19 +55,24 @@ struct KParams {
   uint32_t image_words;
   uint32_t use_pages;          // 1 => 64K lookups go to `pages`
   uint32_t eth_base, tcp_base, udp_base;  // word offsets of the hashes inside `image`
-  uint32_t eth_bits, tcp_bits, udp_bits;  // log2 of each hash's slot count
+  uint32_t eth_bits, tcp_bits, udp_bits;  // log2 of each hash's bucket count
+  uint32_t eth_mult, tcp_mult, udp_mult;  // each hash's multiplier (odd, < 2^16)
   uint32_t first;
   uint32_t decoders;
   uint32_t options;
   uint32_t stage;              // LDS window bytes per buffer (chosen by the runtime)
+  uint32_t nstores;            // store instructions per tile (non-NULL result arrays)
 };
+
+// One launch covers at most this many packets, so packet and tile indices are 32-bit.
+constexpr uint64_t kMaxLaunchPackets = 1ull << 30;
 
 // Launch the decode kernel over P (asynchronous on `stream`).
 hipError_t launch_decode(const KParams &P, hipStream_t stream, int num_cus);
 
-// Fibonacci hash of a 16-bit key into 2^bits slots (host and device must agree).
-__host__ __device__ inline uint32_t key_hash(uint32_t key, uint32_t bits) {
-  return ((key * 40503u) & 0xFFFFu) >> (16 - bits);
+// Multiplicative hash of a 16-bit key into 2^bits buckets (host and device must agree).
+__host__ __device__ inline uint32_t key_hash(uint32_t key, uint32_t mult, uint32_t bits) {
+  return ((key * mult) & 0xFFFFu) >> (16 - bits);
 }
 
 }  // namespace gpd

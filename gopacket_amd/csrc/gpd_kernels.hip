@@ -52,17 +52,19 @@ __device__ __forceinline__ uint32_t lds_u32(uint32_t a) {
 __device__ __forceinline__ uint32_t swz_slot(uint32_t g) { return (g & ~15u) | ((g + (g >> 4)) & 15u); }
 __device__ __forceinline__ uint32_t unswz_slot(uint32_t s) { return (s & ~15u) | ((s - (s >> 4)) & 15u); }
 
+// SWZ: the window's 16-byte slots are rotated (see the file comment); otherwise linear.
+template <bool SWZ>
 struct LdsSrc {
   uint32_t buf;  // LDS byte address of the window
   uint32_t pos;  // logical offset of the packet's first byte in the window
   __device__ __forceinline__ uint32_t abs(uint32_t rel) const { return pos + rel; }
   __device__ __forceinline__ uint32_t phys(uint32_t x) const {
-    return buf + (swz_slot(x >> 4) << 4) + (x & 15u);
+    return SWZ ? buf + (swz_slot(x >> 4) << 4) + (x & 15u) : buf + x;
   }
   __device__ __forceinline__ uint32_t dw(uint32_t x) const { return lds_u32(phys(x)); }  // x 4-aligned
   __device__ __forceinline__ uint32_t u8(uint32_t rel) const { return g_lds[phys(pos + rel)]; }
   __device__ __forceinline__ uint4 q(uint32_t x) const {  // x 16-aligned
-    return *reinterpret_cast<const uint4 *>(g_lds + buf + (swz_slot(x >> 4) << 4));
+    return *reinterpret_cast<const uint4 *>(g_lds + phys(x));
   }
 };
 
@@ -115,7 +117,7 @@ struct TE {        // a dispatch-table result
 template <bool PAGES>
 struct Tab {
   const uint16_t *pages;
-  uint32_t eth_base, tcp_base, udp_base, eth_bits, tcp_bits, udp_bits;
+  uint32_t eth_base, tcp_base, udp_base, eth_bits, tcp_bits, udp_bits, eth_mult, tcp_mult, udp_mult;
 
   // type LUT (registered set applied by the host)
   __device__ __forceinline__ uint32_t lut(uint32_t t) const { return t < 128 ? g_lds[t] : 0xFFu; }
@@ -123,15 +125,17 @@ struct Tab {
     const uint32_t v = lds_u32(4 * (kHashLutWords + (p & 0xFFu)));
     return TE{v & 0xFFFFu, v >> 16};
   }
-  __device__ __forceinline__ TE hash(uint32_t base, uint32_t bits, uint32_t key) const {
-    const uint32_t mask = (1u << bits) - 1;
-    uint32_t h = key_hash(key, bits);
-    for (;;) {  // linear probing; an empty slot ends it (the host bounds probes at 8)
-      const uint32_t v = lds_u32(4 * (base + h));
-      if (v == 0) return TE{0u, 0xFFu};
-      if ((v >> 16) == key) return TE{(v >> 8) & 0xFFu, v & 0xFFu};
-      h = (h + 1) & mask;
-    }
+  // Raw slot of `key` in a two-way bucketed hash: LayerType << 8 | LUT entry in the low 16
+  // bits (0x00FF on a miss: LayerType 0, not registered).  One ds_read_b64, no loop.
+  __device__ __forceinline__ uint32_t bucket(uint32_t base, uint32_t mult, uint32_t bits,
+                                             uint32_t key) const {
+    const uint32_t b = __builtin_amdgcn_ubfe(key * mult, 16 - bits, bits);
+    const uint2 v = *reinterpret_cast<const uint2 *>(g_lds + 4 * base + 8 * b);
+    return (v.x >> 16) == key ? v.x : ((v.y >> 16) == key ? v.y : 0xFFu);
+  }
+  __device__ __forceinline__ TE hash(uint32_t base, uint32_t mult, uint32_t bits, uint32_t key) const {
+    const uint32_t r = bucket(base, mult, bits, key);
+    return TE{(r >> 8) & 0xFFu, r & 0xFFu};
   }
   __device__ __forceinline__ TE page(uint32_t dir, uint32_t key) const {
     const uint32_t pg = pages[dir + (key >> 8)];
@@ -139,13 +143,13 @@ struct Tab {
     return TE{lt, lut(lt)};
   }
   __device__ __forceinline__ TE eth(uint32_t et) const {  // enums_generated.go:77-79
-    return PAGES ? page(kTabEthDir, et) : hash(eth_base, eth_bits, et);
+    return PAGES ? page(kTabEthDir, et) : hash(eth_base, eth_mult, eth_bits, et);
   }
   __device__ __forceinline__ TE tcp(uint32_t port) const {  // ports.go:54-60 (raw)
-    return PAGES ? page(kTabTcpDir, port) : hash(tcp_base, tcp_bits, port);
+    return PAGES ? page(kTabTcpDir, port) : hash(tcp_base, tcp_mult, tcp_bits, port);
   }
   __device__ __forceinline__ TE udp(uint32_t port) const {  // ports.go:97-103 (raw)
-    return PAGES ? page(kTabUdpDir, port) : hash(udp_base, udp_bits, port);
+    return PAGES ? page(kTabUdpDir, port) : hash(udp_base, udp_mult, udp_bits, port);
   }
 };
 
@@ -553,55 +557,169 @@ done:
 // Straight-line decode of the stacks that carry nearly all traffic:
 //   Ethernet [Dot1Q]{0,2} (IPv4 with IHL 5 | IPv6 without hop-by-hop) (TCP | UDP) [Payload]
 // for a 16-byte-aligned packet in an LDS window, with Ethernet as the first layer.  The
-// first 80 bytes come in with five ds_read_b128 (conflict-free on the rotated window) and
-// every header field is extracted at a compile-time offset.  It returns false — having
-// written nothing — as soon as a packet leaves that envelope (options on IPv4, fragments,
-// HBH, VXLAN, any decode error, unusual table mappings...), and the caller then runs the
-// generic decoder, so results are those of decode_packet in every case.
-template <int O, int N>
-__device__ __forceinline__ uint32_t word_at(const uint32_t (&h)[N]) {
-  static_assert(O / 4 + 1 < N || O % 4 == 0, "window");
-  if constexpr (O % 4 == 0) return h[O / 4];
-  else return __builtin_amdgcn_alignbyte(h[O / 4 + 1], h[O / 4], O % 4);
+// first 80 bytes come in with five ds_read_b128 and every header field is read at a
+// compile-time byte position.  A lane whose packet leaves that envelope (IPv4 options,
+// fragments, hop-by-hop, VXLAN, any decode error, unusual table mappings...) returns false
+// having written nothing, and the caller runs the generic decoder on it, so the results are
+// those of decode_packet in every case.
+//
+// Instruction economy (the kernel is VALU-issue bound once the bytes are in LDS):
+//  * checksums are summed in the little-endian domain with v_dot2_u32_u16 (one op per
+//    4 bytes, no byte shuffles) and converted once at the end (fold_le_not);
+//  * FNV-1a multiplies use the 2^40 + 0x1b3 split in three 32-bit ops per byte, with the
+//    first byte from the basis in closed form;
+//  * table lookups are one ds_read_b64 of a two-way bucket and two compares.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t dot2(uint32_t x, uint32_t w, uint32_t acc) {
+  return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, x), __builtin_bit_cast(u16x2, w), acc,
+                                false);
 }
-template <int O, int N>
-__device__ __forceinline__ uint32_t fbyte(const uint32_t (&h)[N]) {
+
+// Sum of the little-endian 16-bit halves of packet bytes [A, B) held in h (A, B even and
+// compile-time), leaving out the half at byte X (the IPv4 checksum field).
+template <int A, int B, int X = -1>
+__device__ __forceinline__ uint32_t lesum(const uint32_t (&h)[20], uint32_t acc) {
+  static_assert(A % 2 == 0 && B % 2 == 0 && B <= 80, "halves");
+#pragma unroll
+  for (int k = A / 4; 4 * k < B; k++) {
+    const uint32_t w = ((4 * k >= A && 4 * k + 2 <= B && 4 * k != X) ? 1u : 0u) |
+                       ((4 * k + 2 >= A && 4 * k + 4 <= B && 4 * k + 2 != X) ? 0x10000u : 0u);
+    if (w) acc = dot2(h[k], w, acc);
+  }
+  return acc;
+}
+
+// ~fold(S) (tcpip.go:66-69) from the little-endian-domain sum S' of the same 16-bit words:
+// the one's-complement sum of byte-swapped words is the byte-swapped sum (RFC 1071 §2(B)),
+// exactly — an all-zero input gives 0 in both domains, anything else a value in
+// [1, 0xFFFF] congruent mod 0xFFFF — as long as neither sum wraps 2^32 (true for the
+// <= 16 KiB a fast-path packet spans).  Two folds bring any u32 to <= 0xFFFF.
+__device__ __forceinline__ uint32_t fold_le_not(uint32_t s) {
+  s = (s >> 16) + (s & 0xFFFFu);
+  s = (s >> 16) + (s & 0xFFFFu);
+  return __builtin_amdgcn_perm(0u, ~s, 0x0C0C0001u);  // byte-swap the low half, high half 0
+}
+
+// BE16 / byte of the packet at compile-time position O
+template <int O>
+__device__ __forceinline__ uint32_t fbyte(const uint32_t (&h)[20]) {
   return (h[O / 4] >> (8 * (O % 4))) & 0xFFu;
 }
-template <int O, int N>
-__device__ __forceinline__ uint32_t fbe16(const uint32_t (&h)[N]) {
-  return (fbyte<O>(h) << 8) | fbyte<O + 1>(h);
+template <int O>
+__device__ __forceinline__ uint32_t fbe16(const uint32_t (&h)[20]) {
+  if constexpr (O % 4 == 3) {
+    return (fbyte<O>(h) << 8) | fbyte<O + 1>(h);
+  } else {  // v_perm: byte0 <- O+1, byte1 <- O
+    constexpr uint32_t sel = 0x0C0C0000u | ((uint32_t)(O % 4) << 8) | (uint32_t)(O % 4 + 1);
+    return __builtin_amdgcn_perm(0u, h[O / 4], sel);
+  }
+}
+
+// FNV-1a (flows.go:60-67) on (lo, hi) halves.  h * fnvPrime with fnvPrime = 2^40 + 0x1b3:
+// lo' = lo * 0x1b3, hi' = hi * 0x1b3 + carry + (lo << 8) (mod 2^32).
+struct H64 {
+  uint32_t lo, hi;
+};
+__device__ __forceinline__ H64 fnv_mulp(H64 h) {
+  const uint64_t p = (uint64_t)h.lo * 0x1b3u;
+  const uint32_t q = (uint32_t)((uint64_t)h.hi * 0x1b3u + (p >> 32));
+  return H64{(uint32_t)p, q + (h.lo << 8)};
+}
+constexpr uint64_t kFnvC0 = (kFnvBasis & ~0xFFull) * kFnvPrime;  // (basis with byte 0 cleared) * prime
+// fnvHash over NB packet bytes starting at compile-time position O
+template <int O, int NB>
+__device__ __forceinline__ H64 fnv_at(const uint32_t (&h)[20]) {
+  // byte 0 in closed form: (basis ^ b) * prime = C0 + c * 0x1b3 + (c << 40), c = b ^ 0x25
+  const uint32_t c = fbyte<O>(h) ^ (uint32_t)(kFnvBasis & 0xFFu);
+  const uint64_t r = (uint64_t)c * 0x1b3u + kFnvC0;
+  H64 x{(uint32_t)r, (uint32_t)(r >> 32) + (c << 8)};
+#pragma unroll
+  for (int j = 1; j < NB; j++) {
+    x.lo ^= (h[(O + j) / 4] >> (8 * ((O + j) % 4))) & 0xFFu;
+    x = fnv_mulp(x);
+  }
+  return x;
+}
+// Flow.FastHash, flows.go:167-174
+__device__ __forceinline__ uint64_t flow_fast(H64 s, H64 d, uint32_t ept) {
+  const uint64_t sum = (((uint64_t)s.hi << 32) | s.lo) + (((uint64_t)d.hi << 32) | d.lo);
+  const H64 x = fnv_mulp(H64{(uint32_t)sum ^ ept, (uint32_t)(sum >> 32)});
+  return ((uint64_t)x.hi << 32) | x.lo;
 }
 
 struct Fast {
   uint32_t truncated, ncount, stop, net, tp;  // net: 1 v4 / 2 v6; tp: 1 TCP / 2 UDP
   uint64_t codes;
-  uint32_t cs;        // ip4 header checksum (low 16)
-  uint32_t ps;        // pseudo-header partial sum of the network layer
-  uint64_t nhash;
+  uint32_t ipsum;     // IPv4 header, LE domain (checksum field left out)
+  uint32_t ps;        // pseudo-header address words, LE domain
+  uint32_t seg_sum;   // transport header + payload, LE domain
+  uint32_t seg_len;
+  uint64_t nhash, thash;
 };
 
 struct FastCtx {        // wave-uniform facts about the registered set
   uint32_t eth_code;    // layer code of Ethernet
   uint32_t dq_code;     // layer code of Dot1Q
   bool dq;              // Dot1Q registered
-  uint32_t pl_ent;      // LUT entry of Payload
+  uint32_t pl_raw;      // Payload as a raw slot: LayerType 2 << 8 | its LUT entry
+  bool cs, hash;        // checksums / flow hashes requested (options)
 };
 
+// LE-domain sum of packet bytes [T4, e) where e >= T4 + MINLEN is a runtime end: the words
+// below T4 + MINLEN statically, the rest of the 80 register bytes one word at a time with a
+// select, a ragged last word from LDS, and bytes past 80 in 16-byte LDS chunks.
+template <int T4, int MINLEN, bool SWZ>
+__device__ __forceinline__ uint32_t seg_lesum(const LdsSrc<SWZ> &s, const uint32_t (&h)[20],
+                                              uint32_t e) {
+  constexpr int S = (T4 + MINLEN) & ~3;  // [T4, S) is always inside the segment
+  uint32_t acc = lesum<T4, S>(h, 0u);
+#pragma unroll
+  for (int k = S / 4; k < 20; k++) acc = dot2(e >= 4u * k + 4u ? h[k] : 0u, 0x00010001u, acc);
+  if (__builtin_expect(e & 3u, 0) && e < 80u) {  // ragged end inside the register window
+    const uint32_t x = s.dw(s.pos + (e & ~3u));
+    acc = dot2(__builtin_amdgcn_ubfe(x, 0, 8u * (e & 3u)), 0x00010001u, acc);
+  }
+  if (__builtin_expect(e > 80u, 0)) {
+    uint32_t x = 80;
+    for (; x + 16u <= e; x += 16u) {
+      const uint4 v = s.q(s.pos + x);
+      acc = dot2(v.x, 0x00010001u, acc);
+      acc = dot2(v.y, 0x00010001u, acc);
+      acc = dot2(v.z, 0x00010001u, acc);
+      acc = dot2(v.w, 0x00010001u, acc);
+    }
+    if (x < e) {
+      const uint4 v = s.q(s.pos + x);
+      const uint32_t r = e - x;  // 1..15 bytes
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint32_t m = r >= 4u * j + 4u ? w[j]
+                         : (r > 4u * j ? __builtin_amdgcn_ubfe(w[j], 0, 8u * (r - 4u * j)) : 0u);
+        acc = dot2(m, 0x00010001u, acc);
+      }
+    }
+  }
+  return acc;
+}
+
+// TCP/UDP NextLayerType on raw slots (tcp.go:308-314, udp.go:105-110): the dst-port entry
+// unless it is 0 or Payload, else the src-port entry (0 => Payload).
+__device__ __forceinline__ uint32_t ports_next_raw(uint32_t rd, uint32_t rs, uint32_t pl_raw) {
+  const uint32_t s = (rs & 0xFF00u) ? rs : pl_raw;
+  return (rd & 0xFD00u) ? rd : s;
+}
+
 // Transport at compile-time offset T4 with `tl` bytes available (the network payload).
-template <int T4, bool PAGES>
-__device__ __forceinline__ bool fast_tp(const LdsSrc &s, const uint32_t (&h)[20], uint32_t tl,
-                                        uint32_t dec, uint32_t code, const Tab<PAGES> &T,
-                                        const FastCtx &F, Fast &f, uint32_t &seg_sum,
-                                        uint32_t &seg_len, uint64_t &thash) {
-  TE next;
-  uint32_t plen;
+template <int T4, bool SWZ>
+__device__ __forceinline__ bool fast_tp(const LdsSrc<SWZ> &s, const uint32_t (&h)[20], uint32_t tl,
+                                        uint32_t dec, uint32_t code, const Tab<false> &T,
+                                        const FastCtx &F, Fast &f) {
+  uint32_t next, plen;
   if (dec == D_TCP) {  // tcp.go:229-314
-    if (tl < 20) return false;
-    const uint32_t doff = fbyte<T4 + 12>(h) >> 4;
-    if (doff < 5) return false;
-    const uint32_t ds = doff * 4;
-    if (ds > tl) return false;
+    const uint32_t ds = (fbyte<T4 + 12>(h) >> 4) * 4u;
+    if (tl < 20u || ds < 20u || ds > tl) return false;
     for (uint32_t q = 20; q < ds;) {  // OPTIONS, tcp.go:274-300 (errors -> generic path)
       const uint32_t k = s.u8(T4 + q);
       if (k == 0) break;
@@ -613,130 +731,104 @@ __device__ __forceinline__ bool fast_tp(const LdsSrc &s, const uint32_t (&h)[20]
       }
       q += ol;
     }
-    next = ports_next(T.tcp(fbe16<T4 + 2>(h)), T.tcp(fbe16<T4>(h)), F.pl_ent);
+    next = ports_next_raw(T.bucket(T.tcp_base, T.tcp_mult, T.tcp_bits, fbe16<T4 + 2>(h)),
+                          T.bucket(T.tcp_base, T.tcp_mult, T.tcp_bits, fbe16<T4>(h)), F.pl_raw);
     plen = tl - ds;
-    seg_len = tl;
+    f.seg_len = tl;
+    if (F.cs) f.seg_sum = seg_lesum<T4, 20>(s, h, T4 + tl);
   } else {  // UDP, udp.go:30-56
-    if (tl < 8) return false;
     const uint32_t length = fbe16<T4 + 4>(h);
-    uint32_t hl;
-    if (length >= 8) {
-      hl = length;
-      if (hl > tl) { f.truncated = 1; hl = tl; }
-    } else if (length == 0) {
-      hl = tl;
-    } else {
-      return false;
+    if (tl < 8u || (length != 0u && length < 8u)) return false;
+    uint32_t hl = tl;
+    if (length >= 8u) {
+      if (length > tl) f.truncated = 1;
+      else hl = length;
     }
-    next = ports_next(T.udp(fbe16<T4 + 2>(h)), T.udp(fbe16<T4>(h)), F.pl_ent);
-    plen = hl - 8;
-    seg_len = hl;
+    next = ports_next_raw(T.bucket(T.udp_base, T.udp_mult, T.udp_bits, fbe16<T4 + 2>(h)),
+                          T.bucket(T.udp_base, T.udp_mult, T.udp_bits, fbe16<T4>(h)), F.pl_raw);
+    plen = hl - 8u;
+    f.seg_len = hl;
+    if (F.cs) f.seg_sum = seg_lesum<T4, 8>(s, h, T4 + hl);
   }
-  const uint32_t w = word_at<T4>(h);
-  thash = flow_mix(fnv_word(kFnvBasis, w, 2), fnv_word(kFnvBasis, w >> 16, 2), dec == D_TCP ? 4u : 5u);
-  seg_sum = be16_sum(s, T4, seg_len);
+  if (F.hash) f.thash = flow_fast(fnv_at<T4, 2>(h), fnv_at<T4 + 2, 2>(h), dec == D_TCP ? 4u : 5u);
   f.tp = dec == D_TCP ? 1u : 2u;
   f.codes |= (uint64_t)code << (16 + 4 * f.ncount);
   f.ncount++;
   if (plen == 0) return true;
-  if ((next.ent & 15u) == D_NONE) { f.stop = next.lt; return true; }
-  if ((next.ent & 15u) != D_PAYLOAD) return false;  // e.g. VXLAN, a registered app layer
-  f.codes |= (uint64_t)(next.ent >> 4) << (16 + 4 * f.ncount);  // Payload consumes the rest
+  const uint32_t nd = next & 15u;
+  if (nd == D_NONE) { f.stop = (next >> 8) & 0xFFu; return true; }
+  if (nd != D_PAYLOAD) return false;  // e.g. VXLAN, a registered app layer
+  f.codes |= (uint64_t)((next >> 4) & 15u) << (16 + 4 * f.ncount);  // Payload consumes the rest
   f.ncount++;
   return true;
 }
 
-// Network layer at compile-time offset L3; `typ` is the LayerType Ethernet/Dot1Q chose.
-template <int L3, bool PAGES>
-__device__ __forceinline__ bool fast_l3(const LdsSrc &s, const uint32_t (&h)[20], uint32_t len,
-                                        TE typ, const Tab<PAGES> &T, const FastCtx &F, Fast &f,
-                                        uint32_t &seg_sum, uint32_t &seg_len, uint64_t &thash) {
-  const uint32_t ent = typ.ent;
-  const uint32_t dec = ent & 15u;
+// Network layer at compile-time offset L3; `raw` is the slot Ethernet/Dot1Q looked up.
+template <int L3, bool SWZ>
+__device__ __forceinline__ bool fast_l3(const LdsSrc<SWZ> &s, const uint32_t (&h)[20], uint32_t len,
+                                        uint32_t raw, const Tab<false> &T, const FastCtx &F,
+                                        Fast &f) {
+  const uint32_t dec = raw & 15u;
   const uint32_t dl = len - L3;
-  TE next;
-  uint32_t plen;
+  uint32_t pv, plen;  // proto-table word of the next header; network payload length
   if (dec == D_IP4) {  // ip4.go:188-286
-    if (dl < 20) return false;
-    const uint32_t w0 = word_at<L3>(h), w1 = word_at<L3 + 4>(h), w2 = word_at<L3 + 8>(h);
-    const uint32_t w3 = word_at<L3 + 12>(h), w4 = word_at<L3 + 16>(h);
-    if ((w0 & 0x0Fu) != 5u) return false;  // IHL != 5: options walk in the generic path
-    const uint32_t length = ((w0 >> 8) & 0xFF00u) | (w0 >> 24);
-    if (length < 20) return false;          // 0 (TSO rule) or an error: generic path
-    const uint32_t ff = ((w1 >> 8) & 0xFF00u) | (w1 >> 24);
-    if (ff & 0x3FFFu) return false;         // MF or fragment offset: Fragment, generic path
+    const uint32_t length = fbe16<L3 + 2>(h);
+    // IHL 5 only (options: generic path); Length 0 (TSO rule) and errors: generic path;
+    // MF or a fragment offset: Fragment, generic path
+    if (dl < 20u || (fbyte<L3>(h) & 0x0Fu) != 5u || length < 20u || (fbe16<L3 + 6>(h) & 0x3FFFu))
+      return false;
     uint32_t dlen = dl;
     if (dl > length) dlen = length;
     else if (dl < length) f.truncated = 1;
-    plen = dlen - 20;
-    next = T.proto((w2 >> 8) & 0xFFu);
-    // checksum(ip4.Contents), ip4.go:158-179 (bytes 10-11 as zero)
-    const uint32_t w2z = w2 & 0x0000FFFFu;
-    uint32_t E = __builtin_amdgcn_udot4(w0, 0x00010001u, 0, false);
-    uint32_t O = __builtin_amdgcn_udot4(w0, 0x01000100u, 0, false);
-    E = __builtin_amdgcn_udot4(w1, 0x00010001u, E, false);
-    O = __builtin_amdgcn_udot4(w1, 0x01000100u, O, false);
-    E = __builtin_amdgcn_udot4(w2z, 0x00010001u, E, false);
-    O = __builtin_amdgcn_udot4(w2z, 0x01000100u, O, false);
-    uint32_t Ea = __builtin_amdgcn_udot4(w3, 0x00010001u, 0, false);
-    uint32_t Oa = __builtin_amdgcn_udot4(w3, 0x01000100u, 0, false);
-    Ea = __builtin_amdgcn_udot4(w4, 0x00010001u, Ea, false);
-    Oa = __builtin_amdgcn_udot4(w4, 0x01000100u, Oa, false);
-    f.cs = fold_not(((E + Ea) << 8) + O + Oa);
-    f.ps = (Ea << 8) + Oa;  // src + dst words of the pseudo-header, tcpip.go:26-35
-    f.nhash = flow_mix(fnv_word(kFnvBasis, w3, 4), fnv_word(kFnvBasis, w4, 4), 1u);
+    plen = dlen - 20u;
+    pv = lds_u32(4 * (kHashLutWords + fbyte<L3 + 9>(h)));
+    if (F.cs) {  // checksum(ip4.Contents), ip4.go:158-179; src/dst shared with the pseudo-header
+      f.ps = lesum<L3 + 12, L3 + 20>(h, 0u);
+      f.ipsum = lesum<L3, L3 + 12, L3 + 10>(h, f.ps);
+    }
+    if (F.hash) f.nhash = flow_fast(fnv_at<L3 + 12, 4>(h), fnv_at<L3 + 16, 4>(h), 1u);
     f.net = 1;
   } else if (dec == D_IP6) {  // ip6.go:221-278 without hop-by-hop
     if constexpr (L3 > 18) {
-      return false;  // transport header would pass the 80-byte register window
+      return false;  // the transport header would pass the 80-byte register window
     } else {
-      if (dl < 40) return false;
-      const uint32_t w1 = word_at<L3 + 4>(h);
-      const uint32_t nh = (w1 >> 16) & 0xFFu;
-      if (nh == 0) return false;
-      const uint32_t length = ((w1 & 0xFFu) << 8) | ((w1 >> 8) & 0xFFu);
-      if (length == 0) return false;
-      plen = dl - 40;
+      const uint32_t nh = fbyte<L3 + 6>(h);
+      const uint32_t length = fbe16<L3 + 4>(h);
+      if (dl < 40u || nh == 0u || length == 0u) return false;
+      plen = dl - 40u;
       if (length > plen) f.truncated = 1;
       else plen = length;
-      next = T.proto(nh);
-      uint64_t hs = kFnvBasis, hd = kFnvBasis;
-      uint32_t E = 0, O = 0;
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const uint32_t a = k == 0 ? word_at<L3 + 8>(h) : k == 1 ? word_at<L3 + 12>(h)
-                         : k == 2 ? word_at<L3 + 16>(h) : word_at<L3 + 20>(h);
-        const uint32_t b = k == 0 ? word_at<L3 + 24>(h) : k == 1 ? word_at<L3 + 28>(h)
-                         : k == 2 ? word_at<L3 + 32>(h) : word_at<L3 + 36>(h);
-        hs = fnv_word(hs, a, 4);
-        hd = fnv_word(hd, b, 4);
-        E = __builtin_amdgcn_udot4(a, 0x00010001u, E, false);
-        O = __builtin_amdgcn_udot4(a, 0x01000100u, O, false);
-        E = __builtin_amdgcn_udot4(b, 0x00010001u, E, false);
-        O = __builtin_amdgcn_udot4(b, 0x01000100u, O, false);
+      pv = lds_u32(4 * (kHashLutWords + nh));
+      if (F.cs) f.ps = lesum<L3 + 8, L3 + 40>(h, 0u);  // tcpip.go:37-48
+      if (F.hash) {
+        H64 hs = fnv_at<L3 + 8, 4>(h), hd = fnv_at<L3 + 24, 4>(h);
+#pragma unroll  // both chains over the remaining 12 address bytes
+        for (int j = 4; j < 16; j++) {
+          hs.lo ^= (h[(L3 + 8 + j) / 4] >> (8 * ((L3 + 8 + j) % 4))) & 0xFFu;
+          hs = fnv_mulp(hs);
+          hd.lo ^= (h[(L3 + 24 + j) / 4] >> (8 * ((L3 + 24 + j) % 4))) & 0xFFu;
+          hd = fnv_mulp(hd);
+        }
+        f.nhash = flow_fast(hs, hd, 2u);
       }
-      f.ps = (E << 8) + O;  // tcpip.go:37-48
-      f.nhash = flow_mix(hs, hd, 2u);
       f.net = 2;
     }
   } else {
     return false;
   }
-  f.codes |= (uint64_t)(ent >> 4) << (16 + 4 * f.ncount);
+  f.codes |= (uint64_t)((raw >> 4) & 15u) << (16 + 4 * f.ncount);
   f.ncount++;
   if (plen == 0) return true;
-  const uint32_t d2 = next.ent & 15u;
-  if (d2 == D_NONE) { f.stop = next.lt; return true; }
+  const uint32_t ent = pv >> 16, d2 = ent & 15u;
+  if (d2 == D_NONE) { f.stop = pv & 0xFFFFu; return true; }
   if (d2 != D_TCP && d2 != D_UDP) return false;
-  if (dec == D_IP4)
-    return fast_tp<L3 + 20>(s, h, plen, d2, next.ent >> 4, T, F, f, seg_sum, seg_len, thash);
-  if constexpr (L3 <= 18)
-    return fast_tp<L3 + 40>(s, h, plen, d2, next.ent >> 4, T, F, f, seg_sum, seg_len, thash);
+  if (dec == D_IP4) return fast_tp<L3 + 20>(s, h, plen, d2, ent >> 4, T, F, f);
+  if constexpr (L3 <= 18) return fast_tp<L3 + 40>(s, h, plen, d2, ent >> 4, T, F, f);
   return false;
 }
 
-template <bool PAGES>
-__device__ __forceinline__ bool fast_decode(const LdsSrc &s, uint32_t len, const Tab<PAGES> &T,
+template <bool SWZ>
+__device__ __forceinline__ bool fast_decode(const LdsSrc<SWZ> &s, uint32_t len, const Tab<false> &T,
                                             const FastCtx &F, uint32_t options, Out &o) {
   if (len < 14) return false;
   uint32_t h[20];
@@ -745,55 +837,51 @@ __device__ __forceinline__ bool fast_decode(const LdsSrc &s, uint32_t len, const
     const uint4 v = s.q(s.pos + 16 * k);
     h[4 * k] = v.x; h[4 * k + 1] = v.y; h[4 * k + 2] = v.z; h[4 * k + 3] = v.w;
   }
-  Fast f{0, 1, 0, 0, 0, 0, 0, 0, 0};
-  f.codes = (uint64_t)F.eth_code << 16;     // Ethernet, ethernet.go:41-62
+  Fast f{0, 1, 0, 0, 0, (uint64_t)F.eth_code << 16, 0, 0, 0, 0, 0, 0};  // Ethernet, ethernet.go:41-62
   const uint32_t et = fbe16<12>(h);
-  if (et < 0x0600u) return false;            // 802.3 length framing: generic path
-  TE typ = T.eth(et);
-  uint32_t seg_sum = 0, seg_len = 0;
-  uint64_t thash = 0;
+  if (et < 0x0600u) return false;  // 802.3 length framing: generic path
+  uint32_t raw = T.bucket(T.eth_base, T.eth_mult, T.eth_bits, et);
   bool ok;
-  if (typ.lt == GPD_LT_DOT1Q && F.dq) {  // dot1q.go:29-50
-    if (len < 18) return false;
+  if (((raw >> 8) & 0xFFu) == GPD_LT_DOT1Q && F.dq) {  // dot1q.go:29-50
+    if (len <= 18) return false;  // short tag or empty Dot1Q payload: generic path
     f.codes |= (uint64_t)F.dq_code << 20;
     f.ncount = 2;
-    typ = T.eth(fbe16<16>(h));
-    if (typ.lt == GPD_LT_DOT1Q) {
-      if (len < 22) return false;
+    raw = T.bucket(T.eth_base, T.eth_mult, T.eth_bits, fbe16<16>(h));
+    if (((raw >> 8) & 0xFFu) == GPD_LT_DOT1Q) {
+      if (len <= 22) return false;
       f.codes |= (uint64_t)F.dq_code << 24;
       f.ncount = 3;
-      typ = T.eth(fbe16<20>(h));
-      if (typ.lt == GPD_LT_DOT1Q) return false;
-      if (len == 22) return false;  // empty Dot1Q payload: generic path ends the loop there
-      ok = fast_l3<22>(s, h, len, typ, T, F, f, seg_sum, seg_len, thash);
+      raw = T.bucket(T.eth_base, T.eth_mult, T.eth_bits, fbe16<20>(h));
+      if (((raw >> 8) & 0xFFu) == GPD_LT_DOT1Q) return false;
+      ok = fast_l3<22>(s, h, len, raw, T, F, f);
     } else {
-      if (len == 18) return false;
-      ok = fast_l3<18>(s, h, len, typ, T, F, f, seg_sum, seg_len, thash);
+      ok = fast_l3<18>(s, h, len, raw, T, F, f);
     }
   } else {
     if (len == 14) return false;
-    ok = fast_l3<14>(s, h, len, typ, T, F, f, seg_sum, seg_len, thash);
+    ok = fast_l3<14>(s, h, len, raw, T, F, f);
   }
   if (!ok) return false;
   // status / layers / hashes / checksums exactly as decode_packet composes them
-  uint32_t klass = GPD_ST_OK;
-  if (f.stop != 0 && !(options & GPD_OPT_IGNORE_UNSUPPORTED)) klass = GPD_ST_UNSUPPORTED;
+  const uint32_t klass =
+      (f.stop != 0 && !(options & GPD_OPT_IGNORE_UNSUPPORTED)) ? GPD_ST_UNSUPPORTED : GPD_ST_OK;
   uint32_t st = klass | (f.truncated << 2) | (f.ncount << 4);
   uint64_t nh = 0, th = 0;
   uint32_t cs = 0;
-  if (!(options & GPD_OPT_NO_FLOW_HASH)) {
+  if (F.hash) {
     nh = f.nhash;
     st |= (1u << 16) | (f.net << 20);
     if (f.tp) {
-      th = thash;
+      th = f.thash;
       st |= (1u << 17) | ((f.tp == 1 ? 4u : 5u) << 24);
     }
   }
-  if (!(options & GPD_OPT_NO_CHECKSUMS)) {
-    if (f.net == 1) { cs = f.cs; st |= 1u << 18; }
-    if (f.tp) {
-      uint32_t ps = f.ps + (f.tp == 1 ? 6u : 17u) + (seg_len & 0xFFFFu) + (seg_len >> 16);
-      cs |= (uint32_t)fold_not(ps + seg_sum) << 16;
+  if (F.cs) {
+    if (f.net == 1) { cs = fold_le_not(f.ipsum); st |= 1u << 18; }
+    if (f.tp) {  // pseudo-header protocol and length as LE-domain words (seg_len < 2^16 here)
+      const uint32_t ps = f.ps + (f.tp == 1 ? 0x0600u : 0x1100u) +
+                          __builtin_amdgcn_perm(0u, f.seg_len, 0x0C0C0001u);
+      cs |= fold_le_not(ps + f.seg_sum) << 16;
       st |= 1u << 19;
     }
   }
@@ -812,7 +900,7 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
   return v;
 }
 
-__device__ __forceinline__ void store_out(const KParams &P, uint64_t i, const Out &o) {
+__device__ __forceinline__ void store_out(const KParams &P, uint32_t i, const Out &o) {
   P.status[i] = o.status;
   P.layers[i] = o.layers;
   if (P.net_hash) P.net_hash[i] = o.net_hash;
@@ -820,145 +908,196 @@ __device__ __forceinline__ void store_out(const KParams &P, uint64_t i, const Ou
   if (P.csum) P.csum[i] = o.csum;
 }
 
-// The first LDS window of a tile: starts at the first packet that fits a window
-// (16-aligned) and covers every packet lying wholly inside [base, base + STAGE).
+// A window of the batch buffer: bytes [base, base + nbytes) (base 16-aligned).
 struct Window {
   uint32_t base, nbytes;
 };
 
+// The first window of a tile starts at the first pending packet (rounded down to 16) and
+// covers every pending packet lying wholly inside [base, base + STAGE).  Packets normally
+// sit in lane order, so lane 63's end is the extent; a full wave maximum only runs when some
+// lane proves otherwise.
 template <int STAGE>
-__device__ __forceinline__ Window plan_window(bool pending, uint32_t off, uint32_t len) {
+__device__ __forceinline__ Window plan_window(bool pending, uint32_t off, uint32_t end) {
   Window w{0, 0};
   const uint64_t m = __ballot(pending);
   if (m == 0) return w;
-  const uint32_t first_lane = __builtin_ctzll(m);
-  w.base = (uint32_t)__shfl((int)off, first_lane) & ~15u;
-  const bool in = pending && off >= w.base && (uint64_t)off + len <= (uint64_t)w.base + STAGE;
-  const uint32_t need = wave_max(in ? (uint32_t)((uint64_t)off + len - w.base) : 0u);
+  w.base = __builtin_amdgcn_readlane(off, (int)__builtin_ctzll(m)) & ~15u;
+  const bool in = pending && off >= w.base && end - w.base <= (uint32_t)STAGE;
+  const uint32_t x = in ? end - w.base : 0u;
+  uint32_t need = __builtin_amdgcn_readlane(x, 63);
+  if (__any(x > need)) need = __builtin_amdgcn_readfirstlane(wave_max(x));
   w.nbytes = (need + 15u) & ~15u;
   return w;
 }
 
-// One 16-byte LDS-DMA (global_load_lds_dwordx4): lane l's 16 bytes land at LDS
-// lds_base + 16 l.  Issued from inline asm so the compiler's waitcnt pass does not see it:
+// 16-byte LDS-DMA (global_load_lds_dwordx4): lane l's 16 bytes from gbase + voff land at LDS
+// lds + 16 l.  Issued from inline asm so the compiler's waitcnt pass does not see it:
 // otherwise it cannot tell the in-flight DMA into the other window from this window's
 // ds_reads and drains it (vmcnt(0)) before the first one, serialising the prefetch.  Every
-// wait on these loads is therefore explicit (s_waitcnt vmcnt(0) before a window is read).
-__device__ __forceinline__ void glds16(const uint8_t *gsrc, uint32_t lds_base) {
+// wait on these loads is therefore explicit (a counted s_waitcnt vmcnt before a window is
+// read; loads, stores and LDS-DMA retire in issue order, MI355X_MICROARCH.md).
+__device__ __forceinline__ void glds16(const uint8_t *gbase, uint32_t voff, uint32_t lds) {
   uint32_t keep;
   asm volatile(
       "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
+      "s_mov_b32 m0, %3\n\t"
       "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\t"
+      "global_load_lds_dwordx4 %1, %2\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
-      : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_base))
+      : "v"(voff), "s"(gbase), "s"(lds)
       : "memory");
 }
 
-// The window into LDS `buf`: wave instruction c writes physical slots [64c, 64c+64); lane
-// l's source is the logical slot that rotates onto slot 64c+l.
+// Per-lane source offsets of a window: wave instruction c writes physical slots
+// [64c, 64c+64); lane l's source is the logical slot that lands on slot 64c + l — for the
+// rotated layout that depends on c mod 4 only (four per-lane constants).
+template <bool SWZ>
+struct DmaLanes {
+  uint32_t voff[4];
+  __device__ __forceinline__ explicit DmaLanes(uint32_t lane) {
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      voff[j] = SWZ ? 16u * ((lane & 48u) + ((lane - (lane >> 4) - 4u * j) & 15u)) : 16u * lane;
+  }
+};
+
+template <bool SWZ>
 __device__ __forceinline__ void issue_window(const uint8_t *data, const Window &w, uint32_t buf,
-                                             uint32_t lane) {
-  for (uint32_t c = 0; c < w.nbytes; c += 1024u) {
-    const uint32_t g = unswz_slot((c >> 4) + lane);
-    if ((g << 4) < w.nbytes) glds16(data + w.base + (g << 4), buf + c);
+                                             const DmaLanes<SWZ> &L) {
+  for (uint32_t c4 = 0; c4 < w.nbytes; c4 += 4096u) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint32_t c = c4 + 1024u * j;
+      if (c >= w.nbytes) break;
+      if (c + 1024u <= w.nbytes || c + L.voff[j] < w.nbytes) glds16(data + w.base + c, L.voff[j], buf + c);
+    }
   }
 }
 
 // ---------------------------------------------------------------- kernel
-// WAVES waves per workgroup; MINW = waves per SIMD the register allocation must allow.
-template <int STAGE, bool EXT, bool PAGES, int WAVES, int MINW>
-__global__ __launch_bounds__(64 * WAVES, MINW) void decode_kernel(KParams P) {
-  constexpr int kWaves = WAVES, kBlock = 64 * WAVES;
+// Counted wait for this tile's window: everything but the last tile's result stores.
+__device__ __forceinline__ void wait_window(uint32_t nstores) {
+  switch (nstores) {
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+// WAVES waves per workgroup; each wave owns 64-packet tiles t, t + W, ... (grid stride).
+template <int STAGE, bool EXT, bool PAGES, bool SWZ, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void decode_kernel(KParams P) {
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wave = threadIdx.x >> 6;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // stage the dispatch-table image (LUT, ipproto, hashes) into LDS
-  for (uint32_t k = threadIdx.x; k < P.image_words; k += kBlock)
+  for (uint32_t k = threadIdx.x; k < P.image_words; k += 64 * WAVES)
     reinterpret_cast<uint32_t *>(g_lds)[k] = P.image[k];
   __syncthreads();
-  const Tab<PAGES> T{P.pages, P.eth_base, P.tcp_base, P.udp_base, P.eth_bits, P.tcp_bits, P.udp_bits};
+  const Tab<PAGES> T{P.pages,    P.eth_base, P.tcp_base, P.udp_base, P.eth_bits,
+                     P.tcp_bits, P.udp_bits, P.eth_mult, P.tcp_mult, P.udp_mult};
   const uint32_t img = (P.image_words * 4u + 15u) & ~15u;
   const uint32_t bufs = img + wave * 2u * STAGE;
-  const uint64_t ntiles = (P.n + 63) / 64;
-  const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+  const uint32_t n = (uint32_t)P.n;  // <= kMaxLaunchPackets per launch
+  const uint32_t ntiles = (n + 63u) >> 6;
+  const uint32_t nwaves = gridDim.x * WAVES;
+  const uint32_t dlen = (uint32_t)P.data_len;
   const uint32_t fits = (uint32_t)STAGE - 15u;  // a packet of <= fits bytes always fits a window
+  const uint32_t options = P.options & ~(kDiagSkipDecode | kDiagNoWait);
   // the fast path assumes Ethernet first (DecodingLayerParser built with LayerTypeEthernet)
-  const bool fast_ok = !PAGES && P.first == GPD_LT_ETHERNET && (T.lut(GPD_LT_ETHERNET) & 15u) == D_ETH;
+  const bool fast_ok = !PAGES && !EXT && P.first == GPD_LT_ETHERNET &&
+                       (T.lut(GPD_LT_ETHERNET) & 15u) == D_ETH;
   const FastCtx F{T.lut(GPD_LT_ETHERNET) >> 4, T.lut(GPD_LT_DOT1Q) >> 4,
-                  (T.lut(GPD_LT_DOT1Q) & 15u) == D_DOT1Q, T.lut(GPD_LT_PAYLOAD)};
+                  (T.lut(GPD_LT_DOT1Q) & 15u) == D_DOT1Q,
+                  ((uint32_t)GPD_LT_PAYLOAD << 8) | T.lut(GPD_LT_PAYLOAD),
+                  !(options & GPD_OPT_NO_CHECKSUMS), !(options & GPD_OPT_NO_FLOW_HASH)};
+  const DmaLanes<SWZ> L(lane);
+  const Tab<false> &TF = reinterpret_cast<const Tab<false> &>(T);
 
-  uint64_t t = (uint64_t)blockIdx.x * kWaves + wave;
+  uint32_t t = blockIdx.x * WAVES + wave;
   if (t >= ntiles) return;
+  // descriptors of tile u (clamped to the buffer at use)
+  auto desc = [&](uint32_t u, uint32_t &off, uint32_t &len) {
+    const uint32_t i = u * 64u + lane;
+    const bool v = u < ntiles && i < n;
+    off = v ? P.offset[i] : 0u;
+    len = v ? P.caplen[i] : 0u;
+    return v;
+  };
   uint32_t cur = 0;
-  uint64_t i = t * 64 + lane;
-  bool valid = i < P.n;
-  uint32_t off = valid ? P.offset[i] : 0u, len = valid ? P.caplen[i] : 0u;
-  Window W = plan_window<STAGE>(valid && len <= fits, off, len);
-  issue_window(P.data, W, bufs, lane);
-  // descriptors of the next tile
-  uint64_t tn = t + nwaves;
-  uint64_t in_ = tn * 64 + lane;
-  bool valid_n = tn < ntiles && in_ < P.n;
-  uint32_t off_n = valid_n ? P.offset[in_] : 0u, len_n = valid_n ? P.caplen[in_] : 0u;
+  uint32_t off, len;
+  bool valid = desc(t, off, len);
+  off = min(off, dlen);
+  uint32_t end = off + min(len, dlen - off);
+  Window W = plan_window<STAGE>(valid && end - off <= fits, off, end);
+  issue_window<SWZ>(P.data, W, bufs, L);
+  uint32_t tn = t + nwaves, off_n, len_n;
+  bool valid_n = desc(tn, off_n, len_n);
 
   for (;;) {
-    // this tile's window and the next tile's descriptors were issued one decode ago
-    if (!(P.options & kDiagNoWait)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // this tile's window and the next tile's descriptors were issued before the last stores
+    if (!(P.options & kDiagNoWait)) {
+      if (EXT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else wait_window(P.nstores);
+    }
     const bool has_next = tn < ntiles;
     Window Wn{0, 0};
+    uint32_t end_n = 0;
     if (has_next) {  // next tile's first window streams in while this tile decodes
-      Wn = plan_window<STAGE>(valid_n && len_n <= fits, off_n, len_n);
-      issue_window(P.data, Wn, bufs + (cur ^ 1u) * STAGE, lane);
+      off_n = min(off_n, dlen);
+      end_n = off_n + min(len_n, dlen - off_n);
+      Wn = plan_window<STAGE>(valid_n && end_n - off_n <= fits, off_n, end_n);
+      issue_window<SWZ>(P.data, Wn, bufs + (cur ^ 1u) * STAGE, L);
     }
     // descriptors two tiles ahead
-    const uint64_t tnn = tn + nwaves;
-    const uint64_t inn = tnn * 64 + lane;
-    const bool valid_nn = tnn < ntiles && inn < P.n;
-    const uint32_t off_nn = valid_nn ? P.offset[inn] : 0u, len_nn = valid_nn ? P.caplen[inn] : 0u;
+    const uint32_t tnn = tn + nwaves;
+    uint32_t off_nn, len_nn;
+    const bool valid_nn = desc(tnn, off_nn, len_nn);
 
+    const uint32_t i = t * 64u + lane;
     const uint32_t buf = bufs + cur * STAGE;
+    const uint32_t clen = end - off;
     gpd_ext_rec *ext = EXT && valid ? P.ext + i : nullptr;
     bool pending = valid;
     Out o;
-    if (pending && len > fits) {  // larger than a window: straight from global memory
-      o = decode_packet<EXT>(GlbSrc{P.data, off}, len, T, P.first, P.options, ext);
+    if (pending && clen > fits) {  // larger than a window: straight from global memory
+      o = decode_packet<EXT>(GlbSrc{P.data, off}, clen, T, P.first, options, ext);
       store_out(P, i, o);
       pending = false;
     }
     bool firstw = true;
     while (__any(pending)) {
-      if (!firstw) {  // further windows of this tile (rare: tiles wider than a window)
-        W = plan_window<STAGE>(pending, off, len);
+      if (!firstw) {  // further windows of this tile (tiles wider than a window)
+        W = plan_window<STAGE>(pending, off, end);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        issue_window(P.data, W, buf, lane);
+        issue_window<SWZ>(P.data, W, buf, L);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       firstw = false;
-      const bool in = pending && off >= W.base && (uint64_t)off + len <= (uint64_t)W.base + STAGE;
+      const bool in = pending && off >= W.base && end - W.base <= (uint32_t)STAGE;
       if (in && (P.options & kDiagSkipDecode)) {  // diagnostics: data movement only
         o = Out{g_lds[buf + ((off - W.base) & ~15u)], 0, 0, 0, 0};
         store_out(P, i, o);
         pending = false;
       } else if (in) {
-        const LdsSrc src{buf, off - W.base};
+        const LdsSrc<SWZ> src{buf, off - W.base};
         bool done = false;
-        if (!EXT && fast_ok && (src.pos & 15u) == 0) done = fast_decode<PAGES>(src, len, T, F, P.options, o);
-        if (!done) o = decode_packet<EXT>(src, len, T, P.first, P.options, ext);
+        if (fast_ok && (src.pos & 15u) == 0) done = fast_decode<SWZ>(src, clen, TF, F, options, o);
+        if (!done) o = decode_packet<EXT>(src, clen, T, P.first, options, ext);
         store_out(P, i, o);
         pending = false;
       }
     }
     if (!has_next) break;
     t = tn;
-    i = in_;
     valid = valid_n;
     off = off_n;
-    len = len_n;
+    end = end_n;
     W = Wn;
     tn = tnn;
-    in_ = inn;
     valid_n = valid_nn;
     off_n = off_nn;
     len_n = len_nn;
@@ -967,7 +1106,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void decode_kernel(KParams P) {
   }
 }
 
-template <int STAGE, bool EXT, bool PAGES, int WAVES, int MINW>
+template <int STAGE, bool EXT, bool PAGES, bool SWZ, int WAVES>
 static hipError_t launch_t(const KParams &P, hipStream_t stream, int num_cus) {
   const uint64_t ntiles = (P.n + 63) / 64;
   const size_t img = (P.image_words * 4u + 15u) & ~15u;
@@ -977,13 +1116,12 @@ static hipError_t launch_t(const KParams &P, hipStream_t stream, int num_cus) {
   const uint64_t cap = (uint64_t)num_cus * (per_cu ? per_cu : 1) * 4;  // a few tiles per wave
   if (blocks > cap) blocks = cap;
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL((decode_kernel<STAGE, EXT, PAGES, WAVES, MINW>), dim3((unsigned)blocks),
+  hipLaunchKernelGGL((decode_kernel<STAGE, EXT, PAGES, SWZ, WAVES>), dim3((unsigned)blocks),
                      dim3(64 * WAVES), lds, stream, P);
   return hipGetLastError();
 }
 
-// Geometry variants (diagnostic selector GPD_GEOM: 0 = 4 waves/WG, 1 = 2 waves/WG with a
-// 5-waves-per-SIMD register budget, 2 = 4 waves/WG with that budget, 3 = 2 waves/WG).
+// Diagnostic selector GPD_GEOM (A/B only): 0 = rotated windows, 1 = linear windows.
 static int geom() {
   static int g = -1;
   if (g < 0) {
@@ -995,22 +1133,16 @@ static int geom() {
 
 template <bool EXT, bool PAGES>
 static hipError_t launch_s(const KParams &P, hipStream_t stream, int num_cus) {
-  const int g = geom();
-  switch (P.stage) {
-    case 4096:
-      if (g == 1) return launch_t<4096, EXT, PAGES, 2, 5>(P, stream, num_cus);
-      if (g == 2) return launch_t<4096, EXT, PAGES, 4, 5>(P, stream, num_cus);
-      if (g == 3) return launch_t<4096, EXT, PAGES, 2, 1>(P, stream, num_cus);
-      return launch_t<4096, EXT, PAGES, 4, 1>(P, stream, num_cus);
-    default:
-      if (g == 1) return launch_t<8192, EXT, PAGES, 2, 5>(P, stream, num_cus);
-      if (g == 2) return launch_t<8192, EXT, PAGES, 4, 5>(P, stream, num_cus);
-      if (g == 3) return launch_t<8192, EXT, PAGES, 2, 1>(P, stream, num_cus);
-      return launch_t<8192, EXT, PAGES, 4, 1>(P, stream, num_cus);
-  }
+  const bool swz = geom() != 1;
+  if (P.stage == 4096)
+    return swz ? launch_t<4096, EXT, PAGES, true, 4>(P, stream, num_cus)
+               : launch_t<4096, EXT, PAGES, false, 4>(P, stream, num_cus);
+  return swz ? launch_t<8192, EXT, PAGES, true, 4>(P, stream, num_cus)
+             : launch_t<8192, EXT, PAGES, false, 4>(P, stream, num_cus);
 }
 
 hipError_t launch_decode(const KParams &P, hipStream_t stream, int num_cus) {
+  if (P.n > kMaxLaunchPackets) return hipErrorInvalidValue;
   if (P.ext) return P.use_pages ? launch_s<true, true>(P, stream, num_cus)
                                 : launch_s<true, false>(P, stream, num_cus);
   return P.use_pages ? launch_s<false, true>(P, stream, num_cus)
@@ -1024,10 +1156,11 @@ hipError_t launch_decode(const KParams &P, hipStream_t stream, int num_cus) {
 namespace gpd {
 __global__ void probe_fast(KParams P) {
   const uint32_t pos = P.offset[threadIdx.x], len = P.caplen[threadIdx.x];
-  const Tab<false> T{P.pages, P.eth_base, P.tcp_base, P.udp_base, P.eth_bits, P.tcp_bits, P.udp_bits};
+  const Tab<false> T{P.pages,    P.eth_base, P.tcp_base, P.udp_base, P.eth_bits,
+                     P.tcp_bits, P.udp_bits, P.eth_mult, P.tcp_mult, P.udp_mult};
   Out o{};
-  const FastCtx F{1, 2, true, 0xC8};
-  const bool ok = fast_decode<false>(LdsSrc{0, pos}, len, T, F, P.options, o);
+  const FastCtx F{1, 2, true, 0x2C8, true, true};
+  const bool ok = fast_decode<false>(LdsSrc<false>{0, pos}, len, T, F, P.options, o);
   const uint32_t i = threadIdx.x;
   if (ok) store_out(P, i, o);
 }

@@ -100,30 +100,46 @@ void type_lut(uint32_t decoders, uint8_t lut[128]) {
     if (decoders & (1u << e.dec)) lut[e.lt] = (uint8_t)(e.dec | (e.code << 4));
 }
 
-// Open-addressed (linear probing) hash of the nonzero entries of a 64K table, u32 slots
-// {key << 16 | LayerType << 8 | lut[LayerType]}; usable when every LayerType is < 256 and
-// no probe sequence exceeds 8.  Returns log2(slots), or 0 when the table does not qualify.
-uint32_t build_hash(const uint16_t *t, const uint8_t lut[128], uint32_t max_words,
-                    std::vector<uint32_t> &slots) {
+// Two-way bucketed hash of the nonzero entries of a 64K table: 2^bits buckets of two u32
+// slots {key << 16 | LayerType << 8 | lut[LayerType]}, bucket = key_hash(key, mult, bits).
+// The multiplier is searched so that no bucket holds more than two keys, which makes every
+// device lookup one ds_read_b64 and two compares (no probe loop).  Unused slots hold a key
+// absent from the table with "LayerType 0, not registered", so they read as a miss.  Usable
+// when every LayerType is < 256 and some (mult, bits) fits max_words; returns false otherwise.
+bool build_hash(const uint16_t *t, const uint8_t lut[128], uint32_t max_words,
+                std::vector<uint32_t> &slots, uint32_t &mult_out, uint32_t &bits_out) {
   std::vector<uint32_t> keys;
+  std::vector<uint8_t> present(65536, 0);
   for (uint32_t k = 0; k < 65536; k++) {
-    if (t[k] >= 256) return 0;
-    if (t[k]) keys.push_back(k);
+    if (t[k] >= 256) return false;
+    if (t[k]) { keys.push_back(k); present[k] = 1; }
   }
-  for (uint32_t bits = 4; bits <= 16 && (1u << bits) <= max_words; bits++) {
-    const uint32_t n = 1u << bits, mask = n - 1;
-    if (keys.size() * 2 > n) continue;
-    slots.assign(n, 0);
-    bool ok = true;
-    for (uint32_t k : keys) {
-      uint32_t h = gpd::key_hash(k, bits), probe = 0;
-      while (slots[h]) { h = (h + 1) & mask; probe++; }
-      if (probe >= 8) { ok = false; break; }
-      slots[h] = (k << 16) | ((uint32_t)t[k] << 8) | (t[k] < 128 ? lut[t[k]] : 0xFFu);
+  uint32_t absent = 0;
+  while (absent < 65536 && present[absent]) absent++;
+  if (absent == 65536) return false;
+  const uint32_t empty = (absent << 16) | 0xFFu;
+  for (uint32_t bits = 2; bits <= 15 && (2u << bits) <= max_words; bits++) {
+    const uint32_t nb = 1u << bits;
+    if (keys.size() > 2 * nb) continue;
+    uint32_t mult = 40503u;  // golden-ratio start, then a fixed odd sequence
+    for (int attempt = 0; attempt < 512; attempt++, mult = (mult * 2654435761u + 0x9E37u) & 0xFFFFu) {
+      mult |= 1u;
+      slots.assign(2 * nb, empty);
+      std::vector<uint8_t> fill(nb, 0);
+      bool ok = true;
+      for (uint32_t k : keys) {
+        const uint32_t b = gpd::key_hash(k, mult, bits);
+        if (fill[b] == 2) { ok = false; break; }
+        slots[2 * b + fill[b]++] = (k << 16) | ((uint32_t)t[k] << 8) | (t[k] < 128 ? lut[t[k]] : 0xFFu);
+      }
+      if (ok) {
+        mult_out = mult;
+        bits_out = bits;
+        return true;
+      }
     }
-    if (ok) return bits;
   }
-  return 0;
+  return false;
 }
 
 }  // namespace
@@ -138,6 +154,7 @@ struct gpd_ctx {
   uint16_t *d_pages = nullptr;  // PAGES fallback
   uint32_t image_words = 0, use_pages = 0;
   uint32_t eth_base = 0, tcp_base = 0, udp_base = 0, eth_bits = 0, tcp_bits = 0, udp_bits = 0;
+  uint32_t eth_mult = 0, tcp_mult = 0, udp_mult = 0;
   bool timing = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
@@ -188,20 +205,23 @@ int gpd_ctx_reload_tables(gpd_ctx *ctx, const gpd_config *cfg) {
   }
   std::vector<uint32_t> he, ht, hu;
   const uint32_t room = gpd::kHashMaxWords - (uint32_t)img.size();
-  uint32_t be = build_hash(eth.data(), lut, room / 2, he);  // 0 => PAGES mode
-  uint32_t bt = be ? build_hash(tcp.data(), lut, room / 4, ht) : 0;
-  uint32_t bu = bt ? build_hash(udp.data(), lut, room / 4, hu) : 0;
+  uint32_t me = 0, mt = 0, mu = 0, be = 0, bt = 0, bu = 0;
+  const bool hashed = build_hash(eth.data(), lut, room / 2, he, me, be) &&
+                      build_hash(tcp.data(), lut, room / 4, ht, mt, bt) &&
+                      build_hash(udp.data(), lut, room / 4, hu, mu, bu);
   HIP_TRY(hipSetDevice(ctx->device));
   if (ctx->d_image) { HIP_TRY(hipFree(ctx->d_image)); ctx->d_image = nullptr; }
   if (ctx->d_pages) { HIP_TRY(hipFree(ctx->d_pages)); ctx->d_pages = nullptr; }
-  if (be && bt && bu) {
+  if (hashed) {  // every hash starts on an 8-byte boundary (ds_read_b64 buckets)
     ctx->use_pages = 0;
-    ctx->eth_base = (uint32_t)img.size(); ctx->eth_bits = be;
-    img.insert(img.end(), he.begin(), he.end());
-    ctx->tcp_base = (uint32_t)img.size(); ctx->tcp_bits = bt;
-    img.insert(img.end(), ht.begin(), ht.end());
-    ctx->udp_base = (uint32_t)img.size(); ctx->udp_bits = bu;
-    img.insert(img.end(), hu.begin(), hu.end());
+    auto put = [&](const std::vector<uint32_t> &h, uint32_t &base) {
+      if (img.size() & 1) img.push_back(0);
+      base = (uint32_t)img.size();
+      img.insert(img.end(), h.begin(), h.end());
+    };
+    put(he, ctx->eth_base); ctx->eth_bits = be; ctx->eth_mult = me;
+    put(ht, ctx->tcp_base); ctx->tcp_bits = bt; ctx->tcp_mult = mt;
+    put(hu, ctx->udp_base); ctx->udp_bits = bu; ctx->udp_mult = mu;
   } else {
     ctx->use_pages = 1;
     std::vector<uint16_t> blob = encode_tables(eth.data(), proto.data(), tcp.data(), udp.data());
@@ -332,15 +352,30 @@ static int launch(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, hipS
   P.use_pages = ctx->use_pages;
   P.eth_base = ctx->eth_base; P.tcp_base = ctx->tcp_base; P.udp_base = ctx->udp_base;
   P.eth_bits = ctx->eth_bits; P.tcp_bits = ctx->tcp_bits; P.udp_bits = ctx->udp_bits;
+  P.eth_mult = ctx->eth_mult; P.tcp_mult = ctx->tcp_mult; P.udp_mult = ctx->udp_mult;
   // LDS window per buffer: the smallest of 4/8 KiB that holds a typical 64-packet tile
   const uint64_t mean_slot = (in->data_len + in->n - 1) / in->n;
   P.stage = mean_slot * 64 <= 4096 ? 4096u : 8192u;
   P.first = ctx->first;
   P.decoders = ctx->decoders;
   P.options = ctx->options;
+  P.nstores = 2u + (out->net_hash != nullptr) + (out->tp_hash != nullptr) + (out->csum != nullptr);
   if (record) HIP_TRY(hipEventRecord(ctx->ev0, stream));
-  hipError_t e = gpd::launch_decode(P, stream, ctx->num_cus);
-  if (e != hipSuccess) return set_err(GPD_ERR_HIP, "decode kernel launch: %s", hipGetErrorString(e));
+  // launches of <= kMaxLaunchPackets packets keep every packet/tile index 32-bit in the kernel
+  for (uint64_t lo = 0; lo < in->n; lo += gpd::kMaxLaunchPackets) {
+    gpd::KParams Q = P;
+    Q.n = std::min<uint64_t>(gpd::kMaxLaunchPackets, in->n - lo);
+    Q.offset = in->offset + lo;
+    Q.caplen = in->caplen + lo;
+    Q.status = out->status + lo;
+    Q.layers = out->layers + lo;
+    Q.net_hash = out->net_hash ? out->net_hash + lo : nullptr;
+    Q.tp_hash = out->tp_hash ? out->tp_hash + lo : nullptr;
+    Q.csum = out->csum ? out->csum + lo : nullptr;
+    Q.ext = out->ext ? out->ext + lo : nullptr;
+    hipError_t e = gpd::launch_decode(Q, stream, ctx->num_cus);
+    if (e != hipSuccess) return set_err(GPD_ERR_HIP, "decode kernel launch: %s", hipGetErrorString(e));
+  }
   if (record) {
     HIP_TRY(hipEventRecord(ctx->ev1, stream));
     ctx->timed = true;
