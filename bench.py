@@ -74,6 +74,49 @@ def cpu_baseline(batch, budget_s: float = 10.0, max_threads: int = 16):
                       f"{threads} threads)"}
 
 
+def dist_max(values, dist, device):
+    """Max over ranks of a few floats (identity without torch.distributed)."""
+    if not dist:
+        return [float(v) for v in values]
+    import torch
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(v) for v in t.cpu()]
+
+
+def summarize(workload, n, world, steps, warmup, elapsed, kern_ms, kern_ms_max, batch, n_err):
+    """The contract JSON object: `value` = packets all ranks decoded / max-over-ranks time."""
+    total_pkts = n * world * steps
+    value = total_pkts / elapsed / 1e6
+    read_bytes = int(batch.caplen.astype(np.int64).sum()) + DESC_BYTES * n
+    write_bytes = 4 + 8 + 8 + 8 + 4  # status, layers, net_hash, tp_hash, csum per packet
+    achieved = read_bytes / (kern_ms * 1e-3) / 1e9
+    return {
+        "metric": "Mpackets/s device-resident Eth/IP/TCP decode+cksum+flow-hash; GB/s vs HBM peak",
+        "value": round(value, 2),
+        "unit": "Mpackets/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": round(elapsed / steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic",
+        "config": {"workload": workload, "packets_per_gpu": n, "parallelism": f"shard{world}",
+                   "read_bytes_per_packet": round(read_bytes / n, 2),
+                   "result_bytes_per_packet": write_bytes,
+                   "decode_errors_in_batch": n_err},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel_ms": round(kern_ms, 4), "kernel_ms_max_rank": round(kern_ms_max, 4),
+                     "algorithmic_bytes_per_launch": read_bytes,
+                     "total_frac_with_results": round((read_bytes + write_bytes * n) /
+                                                      (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -155,46 +198,13 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    if dist:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms_max = float(t[0]), float(t[1])
-    else:
-        kern_ms_max = kern_ms
+    elapsed, kern_ms_max = dist_max([elapsed, kern_ms], dist, f"cuda:{local}")
 
     # correctness guard on what was measured (cheap: status classes only)
     st = dev_res.status.cpu().numpy().view(np.uint32)
     n_err = int(np.count_nonzero((st & 3) != 0))
-
-    total_pkts = n * world * args.steps
-    value = total_pkts / elapsed / 1e6
-    read_bytes = int(batch.caplen.astype(np.int64).sum()) + DESC_BYTES * n
-    write_bytes = 4 + 8 + 8 + 8 + 4  # status, layers, net_hash, tp_hash, csum per packet
-    achieved = read_bytes / (kern_ms * 1e-3) / 1e9
-    out = {
-        "metric": "Mpackets/s device-resident Eth/IP/TCP decode+cksum+flow-hash; GB/s vs HBM peak",
-        "value": round(value, 2),
-        "unit": "Mpackets/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u8",
-        "data": "synthetic",
-        "config": {"workload": workload, "packets_per_gpu": n, "parallelism": f"shard{world}",
-                   "read_bytes_per_packet": round(read_bytes / n, 2),
-                   "result_bytes_per_packet": write_bytes,
-                   "decode_errors_in_batch": n_err},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel_ms": round(kern_ms, 4), "kernel_ms_max_rank": round(kern_ms_max, 4),
-                     "algorithmic_bytes_per_launch": read_bytes,
-                     "total_frac_with_results": round((read_bytes + write_bytes * n) /
-                                                      (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
-    }
+    out = summarize(workload, n, world, args.steps, args.warmup, elapsed, kern_ms, kern_ms_max,
+                    batch, n_err)
     if args.ablate:
         out["ablation"] = args.ablate
         out["metric"] = "DIAGNOSTIC ablation (not the metric): " + out["metric"]

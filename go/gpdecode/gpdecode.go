@@ -1,0 +1,308 @@
+// Package gpdecode is the cgo binding a gopacket maintainer would add to run
+// DecodingLayerParser batches on an MI355X through libgpd.so (include/gpd.h).
+//
+// It mirrors gopacket's parser surface (parser.go:182-350) with batch entry
+// points: one DecodeBatch call decodes every packet of a PacketBatch in one
+// kernel launch, then per-index accessors return what DecodeLayers, Truncated,
+// NetworkFlow().FastHash(), TransportFlow().FastHash(), the IPv4 header checksum
+// and TCP.ComputeChecksum() would have returned for that packet.
+//
+// NOTE: this image has no Go toolchain, so this file is not compiled or tested in
+// this repository. The C-ABI it binds is exercised by the Python ctypes binding
+// (gopacket_amd/_lib.py) and tests/test_parity_gpu.py.
+package gpdecode
+
+/*
+#cgo CFLAGS: -I${SRCDIR}/../../include
+#cgo LDFLAGS: -L${SRCDIR}/../../gopacket_amd -lgpd -Wl,-rpath,${SRCDIR}/../../gopacket_amd
+#include <stdlib.h>
+#include "gpd.h"
+*/
+import "C"
+
+import (
+	"errors"
+	"fmt"
+	"runtime"
+	"unsafe"
+
+	"github.com/google/gopacket"
+	"github.com/google/gopacket/layers"
+)
+
+// Decoder bits: which DecodingLayers are registered (gpd.h GPD_DEC_*).
+const (
+	DecEthernet   = C.GPD_DEC_ETHERNET
+	DecDot1Q      = C.GPD_DEC_DOT1Q
+	DecIPv4       = C.GPD_DEC_IPV4
+	DecIPv6       = C.GPD_DEC_IPV6
+	DecIPv6Ext    = C.GPD_DEC_IPV6_EXT
+	DecTCP        = C.GPD_DEC_TCP
+	DecUDP        = C.GPD_DEC_UDP
+	DecVXLAN      = C.GPD_DEC_VXLAN
+	DecPayload    = C.GPD_DEC_PAYLOAD
+	DecFragment   = C.GPD_DEC_FRAGMENT
+	DecAll        = C.GPD_DEC_ALL
+	optIgnoreUnsp = C.GPD_OPT_IGNORE_UNSUPPORTED
+	optIgnorePan  = C.GPD_OPT_IGNORE_PANIC
+)
+
+// decoderBit maps the DecodingLayer values a caller already builds for
+// gopacket.NewDecodingLayerParser to the engine's decoder bits.
+func decoderBit(d gopacket.DecodingLayer) (uint32, error) {
+	switch d.(type) {
+	case *layers.Ethernet:
+		return DecEthernet, nil
+	case *layers.Dot1Q:
+		return DecDot1Q, nil
+	case *layers.IPv4:
+		return DecIPv4, nil
+	case *layers.IPv6:
+		return DecIPv6, nil
+	case *layers.IPv6ExtensionSkipper:
+		return DecIPv6Ext, nil
+	case *layers.TCP:
+		return DecTCP, nil
+	case *layers.UDP:
+		return DecUDP, nil
+	case *layers.VXLAN:
+		return DecVXLAN, nil
+	case *gopacket.Payload:
+		return DecPayload, nil
+	case *gopacket.Fragment:
+		return DecFragment, nil
+	}
+	return 0, fmt.Errorf("gpdecode: %T has no MI355X decoder", d)
+}
+
+// BatchDecodingLayerParser is the batch form of gopacket.DecodingLayerParser.
+type BatchDecodingLayerParser struct {
+	ctx               *C.gpd_ctx
+	first             gopacket.LayerType
+	decoders          uint32
+	IgnoreUnsupported bool // parser.go:336-350
+	IgnorePanic       bool
+	options           uint32
+}
+
+// NewBatchDecodingLayerParser mirrors gopacket.NewDecodingLayerParser
+// (parser.go:222-233). The dispatch tables (EthernetTypeMetadata,
+// IPProtocolMetadata, the TCP/UDP port maps) are snapshotted when the device
+// context is created; call ReloadTables after layers.Register*PortLayerType.
+func NewBatchDecodingLayerParser(device int, first gopacket.LayerType, decoders ...gopacket.DecodingLayer) (*BatchDecodingLayerParser, error) {
+	p := &BatchDecodingLayerParser{first: first}
+	for _, d := range decoders {
+		bit, err := decoderBit(d)
+		if err != nil {
+			return nil, err
+		}
+		p.decoders |= bit
+	}
+	cfg := C.gpd_config{first_layer: C.uint32_t(first), decoders: C.uint32_t(p.decoders)}
+	if rc := C.gpd_ctx_create(C.int(device), &cfg, &p.ctx); rc != C.GPD_OK {
+		return nil, lastError("gpd_ctx_create", rc)
+	}
+	runtime.SetFinalizer(p, (*BatchDecodingLayerParser).Close)
+	return p, nil
+}
+
+// Close releases the device context.
+func (p *BatchDecodingLayerParser) Close() {
+	if p.ctx != nil {
+		C.gpd_ctx_destroy(p.ctx)
+		p.ctx = nil
+	}
+}
+
+// ReloadTables re-snapshots the reference's global dispatch tables
+// (layers/ports.go:78-80,126-128) into the device context. The tables are
+// passed as flat LayerType arrays; BuildTables shows how to fill them.
+func (p *BatchDecodingLayerParser) ReloadTables(t *Tables) error {
+	cfg := C.gpd_config{
+		first_layer: C.uint32_t(p.first),
+		decoders:    C.uint32_t(p.decoders),
+		ethertype:   (*C.uint16_t)(unsafe.Pointer(&t.EtherType[0])),
+		ipproto:     (*C.uint16_t)(unsafe.Pointer(&t.IPProtocol[0])),
+		tcp_port:    (*C.uint16_t)(unsafe.Pointer(&t.TCPPort[0])),
+		udp_port:    (*C.uint16_t)(unsafe.Pointer(&t.UDPPort[0])),
+	}
+	if rc := C.gpd_ctx_reload_tables(p.ctx, &cfg); rc != C.GPD_OK {
+		return lastError("gpd_ctx_reload_tables", rc)
+	}
+	return nil
+}
+
+// Tables are the four reference tables as LayerType numbers.
+type Tables struct {
+	EtherType  [65536]uint16 // EthernetTypeMetadata[t].LayerType, layers/enums.go:304-321
+	IPProtocol [256]uint16   // IPProtocolMetadata[p].LayerType, layers/enums.go:323-345
+	TCPPort    [65536]uint16 // tcpPortLayerType, layers/ports.go:62-74 (0 => Payload)
+	UDPPort    [65536]uint16 // udpPortLayerType, layers/ports.go:105-122
+}
+
+// BuildTables reads the live gopacket tables.
+func BuildTables() *Tables {
+	t := &Tables{}
+	for i := 0; i < 65536; i++ {
+		t.EtherType[i] = uint16(layers.EthernetTypeMetadata[i].LayerType)
+		t.TCPPort[i] = uint16(layers.TCPPort(i).LayerType())
+		t.UDPPort[i] = uint16(layers.UDPPort(i).LayerType())
+		if t.TCPPort[i] == uint16(gopacket.LayerTypePayload) {
+			t.TCPPort[i] = 0
+		}
+		if t.UDPPort[i] == uint16(gopacket.LayerTypePayload) {
+			t.UDPPort[i] = 0
+		}
+	}
+	for i := 0; i < 256; i++ {
+		t.IPProtocol[i] = uint16(layers.IPProtocolMetadata[i].LayerType)
+	}
+	return t
+}
+
+// PacketBatch holds packets back to back: packet i is
+// Data[Offset[i] : Offset[i]+CapLen[i]]. Data must stay valid until the call
+// returns (gpd_decode_host copies it through pinned staging).
+type PacketBatch struct {
+	Data   []byte
+	Offset []uint32
+	CapLen []uint32
+}
+
+// Append adds one packet (e.g. the data from a pcap.Handle.ReadPacketData loop),
+// 16-byte aligned, the layout the kernel's fast path expects.
+func (b *PacketBatch) Append(pkt []byte) {
+	for len(b.Data)%16 != 0 {
+		b.Data = append(b.Data, 0)
+	}
+	b.Offset = append(b.Offset, uint32(len(b.Data)))
+	b.CapLen = append(b.CapLen, uint32(len(pkt)))
+	b.Data = append(b.Data, pkt...)
+}
+
+// Result is the per-packet SoA the kernel writes (include/gpd.h).
+type Result struct {
+	Status   []uint32
+	Layers   []uint64
+	NetHash  []uint64
+	TpHash   []uint64
+	Checksum []uint32
+}
+
+// DecodeBatch decodes every packet of b (host memory, pinned H2D -> kernel -> D2H).
+func (p *BatchDecodingLayerParser) DecodeBatch(b *PacketBatch) (*Result, error) {
+	n := len(b.Offset)
+	r := &Result{make([]uint32, n), make([]uint64, n), make([]uint64, n), make([]uint64, n), make([]uint32, n)}
+	if n == 0 {
+		return r, nil
+	}
+	// the data buffer must be readable to round_up(len, 16) + 16
+	data := b.Data
+	if cap(data) < len(data)+32 {
+		data = append(make([]byte, 0, len(data)+32), data...)
+	}
+	in := C.gpd_batch{
+		data:     (*C.uint8_t)(unsafe.Pointer(&data[0])),
+		data_len: C.uint64_t(len(b.Data)),
+		offset:   (*C.uint32_t)(unsafe.Pointer(&b.Offset[0])),
+		caplen:   (*C.uint32_t)(unsafe.Pointer(&b.CapLen[0])),
+		n:        C.uint64_t(n),
+	}
+	out := C.gpd_result{
+		status:   (*C.uint32_t)(unsafe.Pointer(&r.Status[0])),
+		layers:   (*C.uint64_t)(unsafe.Pointer(&r.Layers[0])),
+		net_hash: (*C.uint64_t)(unsafe.Pointer(&r.NetHash[0])),
+		tp_hash:  (*C.uint64_t)(unsafe.Pointer(&r.TpHash[0])),
+		csum:     (*C.uint32_t)(unsafe.Pointer(&r.Checksum[0])),
+	}
+	if err := p.configure(); err != nil {
+		return nil, err
+	}
+	if rc := C.gpd_decode_host(p.ctx, &in, &out); rc != C.GPD_OK {
+		return nil, lastError("gpd_decode_host", rc)
+	}
+	runtime.KeepAlive(data)
+	return r, nil
+}
+
+// configure re-creates the context when the parser options changed.
+func (p *BatchDecodingLayerParser) configure() error {
+	var o uint32
+	if p.IgnoreUnsupported {
+		o |= optIgnoreUnsp
+	}
+	if p.IgnorePanic {
+		o |= optIgnorePan
+	}
+	if o == p.options {
+		return nil
+	}
+	cfg := C.gpd_config{first_layer: C.uint32_t(p.first), decoders: C.uint32_t(p.decoders), options: C.uint32_t(o)}
+	var ctx *C.gpd_ctx
+	if rc := C.gpd_ctx_create(0, &cfg, &ctx); rc != C.GPD_OK {
+		return lastError("gpd_ctx_create", rc)
+	}
+	p.Close()
+	p.ctx, p.options = ctx, o
+	return nil
+}
+
+var codeLayerType = [16]gopacket.LayerType{0, layers.LayerTypeEthernet, layers.LayerTypeDot1Q,
+	layers.LayerTypeIPv4, layers.LayerTypeIPv6, layers.LayerTypeIPv6HopByHop,
+	layers.LayerTypeIPv6Routing, layers.LayerTypeIPv6Fragment, layers.LayerTypeIPv6Destination,
+	layers.LayerTypeTCP, layers.LayerTypeUDP, layers.LayerTypeVXLAN,
+	gopacket.LayerTypePayload, gopacket.LayerTypeFragment, 0, 0}
+
+// Decoded fills decoded exactly as DecodeLayers would (parser.go:302-316).
+func (r *Result) Decoded(i int, decoded *[]gopacket.LayerType) {
+	*decoded = (*decoded)[:0]
+	n := int(r.Status[i]>>4) & 31
+	for k := 0; k < n && k < C.GPD_CORE_MAX_LAYERS; k++ {
+		*decoded = append(*decoded, codeLayerType[(r.Layers[i]>>(16+4*uint(k)))&15])
+	}
+}
+
+// Truncated is parser.Truncated after DecodeLayers on packet i.
+func (r *Result) Truncated(i int) bool { return r.Status[i]&4 != 0 }
+
+// Err is DecodeLayers' return value for packet i. Decode errors carry the
+// reference's text when the format has no arguments; the ext record
+// (gpd_ext_rec.err_arg0/1) supplies the arguments otherwise.
+func (r *Result) Err(i int) error {
+	switch r.Status[i] & 3 {
+	case C.GPD_ST_UNSUPPORTED:
+		return gopacket.UnsupportedLayerType(gopacket.LayerType(r.Layers[i] & 0xFFFF))
+	case C.GPD_ST_DECODE_ERROR:
+		return errors.New(errorText[(r.Status[i]>>9)&63])
+	}
+	return nil
+}
+
+// NetworkFlowHash is ip4/ip6.NetworkFlow().FastHash() of the last network layer.
+func (r *Result) NetworkFlowHash(i int) (uint64, bool) { return r.NetHash[i], r.Status[i]&(1<<16) != 0 }
+
+// TransportFlowHash is tcp/udp.TransportFlow().FastHash() of the last transport.
+func (r *Result) TransportFlowHash(i int) (uint64, bool) { return r.TpHash[i], r.Status[i]&(1<<17) != 0 }
+
+// IPv4HeaderChecksum is layers/ip4.go:158 checksum(ip4.Contents): compare with ip4.Checksum.
+func (r *Result) IPv4HeaderChecksum(i int) (uint16, bool) {
+	return uint16(r.Checksum[i]), r.Status[i]&(1<<18) != 0
+}
+
+// TransportChecksum is TCP.ComputeChecksum() (or the same sum over UDP): 0 when valid.
+func (r *Result) TransportChecksum(i int) (uint16, bool) {
+	return uint16(r.Checksum[i] >> 16), r.Status[i]&(1<<19) != 0
+}
+
+var errorText = map[uint32]string{
+	1: "Ethernet packet too small", 7: "Not all IP header bytes available",
+	14: "IPv6 header option too small", 15: "IPv6 header TLV option too small",
+	16: "Jumbo length TLV data must have length 4", 17: "Jumbo length cannot be less than 65536",
+	18: "IPv6 has jumbo length and IPv6 length is not 0",
+	19: "IPv6 length 0, but HopByHop header does not have jumbogram option",
+	23: "TCP data offset greater than packet length", 29: "vxlan packet too small",
+}
+
+func lastError(what string, rc C.int) error {
+	return fmt.Errorf("%s: rc=%d: %s", what, int(rc), C.GoString(C.gpd_last_error_string()))
+}

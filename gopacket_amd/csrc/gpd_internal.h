@@ -32,6 +32,13 @@ namespace gpd {
 constexpr uint32_t kHashLutWords = 32;
 constexpr uint32_t kHashProtoWords = 256;
 constexpr uint32_t kHashMaxWords = 4096;  // 16 KB cap for the LDS image
+// Fixed layout (when the three tables fit it with one shared multiplier): compiled into the
+// fast kernel, so its lookups need no per-table base/size registers.
+constexpr uint32_t kFixBits = 6;
+constexpr uint32_t kFixEthBase = kHashLutWords + kHashProtoWords;  // 288
+constexpr uint32_t kFixTcpBase = kFixEthBase + (2u << kFixBits);     // 416
+constexpr uint32_t kFixUdpBase = kFixTcpBase + (2u << kFixBits);     // 544
+constexpr uint32_t kFixWords = kFixUdpBase + (2u << kFixBits);       // 672
 constexpr uint32_t kTabIpProto = 0;
 constexpr uint32_t kTabEthDir = 256;
 constexpr uint32_t kTabTcpDir = 512;
@@ -62,7 +69,14 @@ struct KParams {
   uint32_t options;
   uint32_t stage;              // LDS window bytes per buffer (chosen by the runtime)
   uint32_t nstores;            // store instructions per tile (non-NULL result arrays)
+  uint32_t fixed;              // tables in the kFix* layout (eth_mult shared by all three)
+  uint32_t *fb_count;          // fast kernel: fallback list length (device scratch)
+  uint32_t *fb_list;           // fast kernel: packet indices left to the generic decoder
 };
+
+// True when launch_decode takes the fast kernel + fallback list (needs fb_count/fb_list
+// with room for P.n entries).
+bool fast_eligible(const KParams &P);
 
 // One launch covers at most this many packets, so packet and tile indices are 32-bit.
 constexpr uint64_t kMaxLaunchPackets = 1ull << 30;

@@ -555,19 +555,23 @@ done:
 
 // ---------------------------------------------------------------- fast path
 // Straight-line decode of the stacks that carry nearly all traffic:
-//   Ethernet [Dot1Q]{0,2} (IPv4 with IHL 5 | IPv6 without hop-by-hop) (TCP | UDP) [Payload]
-// for a 16-byte-aligned packet in an LDS window, with Ethernet as the first layer.  The
-// first 80 bytes come in with five ds_read_b128 and every header field is read at a
-// compile-time byte position.  A lane whose packet leaves that envelope (IPv4 options,
-// fragments, hop-by-hop, VXLAN, any decode error, unusual table mappings...) returns false
-// having written nothing, and the caller runs the generic decoder on it, so the results are
-// those of decode_packet in every case.
+//   Ethernet [Dot1Q]{0,2} (IPv4 with IHL 5 | IPv6 without hop-by-hop) (TCP | UDP)
+//     [Payload | VXLAN + the same stack once more]
+// for a packet in an LDS window, with Ethernet as the first layer.  Header offsets are
+// runtime values and every header is read straight from LDS at its own byte address
+// (gfx950 DS instructions take unaligned addresses), so one code path serves every tag
+// count and both VXLAN passes.  The parse only records where the objects the fused outputs
+// read ended up (the last IPv4 header, the last network layer, the last transport); the
+// checksums and hashes are computed once at the end from LDS.  A lane whose packet leaves
+// the envelope (IPv4 options, fragments, hop-by-hop, any decode error, unusual table
+// mappings...) returns false having written nothing, and the packet goes to the generic
+// decoder, so the results are those of decode_packet in every case.
 //
 // Instruction economy (the kernel is VALU-issue bound once the bytes are in LDS):
 //  * checksums are summed in the little-endian domain with v_dot2_u32_u16 (one op per
 //    4 bytes, no byte shuffles) and converted once at the end (fold_le_not);
-//  * FNV-1a multiplies use the 2^40 + 0x1b3 split in three 32-bit ops per byte, with the
-//    first byte from the basis in closed form;
+//  * FNV-1a multiplies use the 2^40 + 0x1b3 split, with the first byte from the basis in
+//    closed form;
 //  * table lookups are one ds_read_b64 of a two-way bucket and two compares.
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
@@ -576,19 +580,21 @@ __device__ __forceinline__ uint32_t dot2(uint32_t x, uint32_t w, uint32_t acc) {
                                 false);
 }
 
-// Sum of the little-endian 16-bit halves of packet bytes [A, B) held in h (A, B even and
-// compile-time), leaving out the half at byte X (the IPv4 checksum field).
-template <int A, int B, int X = -1>
-__device__ __forceinline__ uint32_t lesum(const uint32_t (&h)[20], uint32_t acc) {
-  static_assert(A % 2 == 0 && B % 2 == 0 && B <= 80, "halves");
-#pragma unroll
-  for (int k = A / 4; 4 * k < B; k++) {
-    const uint32_t w = ((4 * k >= A && 4 * k + 2 <= B && 4 * k != X) ? 1u : 0u) |
-                       ((4 * k + 2 >= A && 4 * k + 4 <= B && 4 * k + 2 != X) ? 0x10000u : 0u);
-    if (w) acc = dot2(h[k], w, acc);
-  }
-  return acc;
-}
+// LDS reads at any byte address
+struct __attribute__((packed, aligned(1))) U128 {
+  uint32_t x, y, z, w;
+};
+struct __attribute__((packed, aligned(1))) U64 {
+  uint32_t x, y;
+};
+typedef uint32_t __attribute__((aligned(1))) U32;
+__device__ __forceinline__ U128 ld128(uint32_t a) { return *reinterpret_cast<const U128 *>(g_lds + a); }
+__device__ __forceinline__ U64 ld64(uint32_t a) { return *reinterpret_cast<const U64 *>(g_lds + a); }
+__device__ __forceinline__ uint32_t ld32(uint32_t a) { return *reinterpret_cast<const U32 *>(g_lds + a); }
+
+// big-endian 16-bit value of bytes (0,1) / (2,3) of a little-endian word
+__device__ __forceinline__ uint32_t be_lo(uint32_t w) { return __builtin_amdgcn_perm(0u, w, 0x0C0C0001u); }
+__device__ __forceinline__ uint32_t be_hi(uint32_t w) { return __builtin_amdgcn_perm(0u, w, 0x0C0C0203u); }
 
 // ~fold(S) (tcpip.go:66-69) from the little-endian-domain sum S' of the same 16-bit words:
 // the one's-complement sum of byte-swapped words is the byte-swapped sum (RFC 1071 §2(B)),
@@ -601,19 +607,29 @@ __device__ __forceinline__ uint32_t fold_le_not(uint32_t s) {
   return __builtin_amdgcn_perm(0u, ~s, 0x0C0C0001u);  // byte-swap the low half, high half 0
 }
 
-// BE16 / byte of the packet at compile-time position O
-template <int O>
-__device__ __forceinline__ uint32_t fbyte(const uint32_t (&h)[20]) {
-  return (h[O / 4] >> (8 * (O % 4))) & 0xFFu;
-}
-template <int O>
-__device__ __forceinline__ uint32_t fbe16(const uint32_t (&h)[20]) {
-  if constexpr (O % 4 == 3) {
-    return (fbyte<O>(h) << 8) | fbyte<O + 1>(h);
-  } else {  // v_perm: byte0 <- O+1, byte1 <- O
-    constexpr uint32_t sel = 0x0C0C0000u | ((uint32_t)(O % 4) << 8) | (uint32_t)(O % 4 + 1);
-    return __builtin_amdgcn_perm(0u, h[O / 4], sel);
+// LE-domain sum of the 16-bit halves of the L bytes at LDS address p (an odd last byte
+// counts as the low byte of its half, i.e. << 8 in the big-endian domain).
+__device__ __forceinline__ uint32_t lesum_lds(uint32_t p, uint32_t L, uint32_t acc) {
+  uint32_t x = 0;
+  for (; x + 16u <= L; x += 16u) {
+    const U128 q = ld128(p + x);
+    acc = dot2(q.x, 0x00010001u, acc);
+    acc = dot2(q.y, 0x00010001u, acc);
+    acc = dot2(q.z, 0x00010001u, acc);
+    acc = dot2(q.w, 0x00010001u, acc);
   }
+  if (x < L) {  // 1..15 ragged bytes: keep the first r of the next 16
+    const U128 q = ld128(p + x);
+    const uint32_t r8 = (L - x) * 8u;
+    uint64_t lo = ((uint64_t)q.y << 32) | q.x, hi = ((uint64_t)q.w << 32) | q.z;
+    lo = r8 >= 64u ? lo : (lo << (64u - r8)) >> (64u - r8);
+    hi = r8 > 64u ? (hi << (128u - r8)) >> (128u - r8) : 0ull;
+    acc = dot2((uint32_t)lo, 0x00010001u, acc);
+    acc = dot2((uint32_t)(lo >> 32), 0x00010001u, acc);
+    acc = dot2((uint32_t)hi, 0x00010001u, acc);
+    acc = dot2((uint32_t)(hi >> 32), 0x00010001u, acc);
+  }
+  return acc;
 }
 
 // FNV-1a (flows.go:60-67) on (lo, hi) halves.  h * fnvPrime with fnvPrime = 2^40 + 0x1b3:
@@ -623,20 +639,27 @@ struct H64 {
 };
 __device__ __forceinline__ H64 fnv_mulp(H64 h) {
   const uint64_t p = (uint64_t)h.lo * 0x1b3u;
-  const uint32_t q = (uint32_t)((uint64_t)h.hi * 0x1b3u + (p >> 32));
-  return H64{(uint32_t)p, q + (h.lo << 8)};
+  return H64{(uint32_t)p, h.hi * 0x1b3u + (uint32_t)(p >> 32) + (h.lo << 8)};
 }
 constexpr uint64_t kFnvC0 = (kFnvBasis & ~0xFFull) * kFnvPrime;  // (basis with byte 0 cleared) * prime
-// fnvHash over NB packet bytes starting at compile-time position O
-template <int O, int NB>
-__device__ __forceinline__ H64 fnv_at(const uint32_t (&h)[20]) {
+// fnvHash of the NB low bytes of w (byte 0 first), from the basis
+template <int NB>
+__device__ __forceinline__ H64 fnv_start(uint32_t w) {
   // byte 0 in closed form: (basis ^ b) * prime = C0 + c * 0x1b3 + (c << 40), c = b ^ 0x25
-  const uint32_t c = fbyte<O>(h) ^ (uint32_t)(kFnvBasis & 0xFFu);
+  const uint32_t c = (w & 0xFFu) ^ (uint32_t)(kFnvBasis & 0xFFu);
   const uint64_t r = (uint64_t)c * 0x1b3u + kFnvC0;
   H64 x{(uint32_t)r, (uint32_t)(r >> 32) + (c << 8)};
 #pragma unroll
   for (int j = 1; j < NB; j++) {
-    x.lo ^= (h[(O + j) / 4] >> (8 * ((O + j) % 4))) & 0xFFu;
+    x.lo ^= (w >> (8 * j)) & 0xFFu;
+    x = fnv_mulp(x);
+  }
+  return x;
+}
+__device__ __forceinline__ H64 fnv_more(H64 x, uint32_t w) {  // four more bytes
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    x.lo ^= (w >> (8 * j)) & 0xFFu;
     x = fnv_mulp(x);
   }
   return x;
@@ -648,60 +671,21 @@ __device__ __forceinline__ uint64_t flow_fast(H64 s, H64 d, uint32_t ept) {
   return ((uint64_t)x.hi << 32) | x.lo;
 }
 
-struct Fast {
-  uint32_t truncated, ncount, stop, net, tp;  // net: 1 v4 / 2 v6; tp: 1 TCP / 2 UDP
-  uint64_t codes;
-  uint32_t ipsum;     // IPv4 header, LE domain (checksum field left out)
-  uint32_t ps;        // pseudo-header address words, LE domain
-  uint32_t seg_sum;   // transport header + payload, LE domain
-  uint32_t seg_len;
-  uint64_t nhash, thash;
-};
-
-struct FastCtx {        // wave-uniform facts about the registered set
-  uint32_t eth_code;    // layer code of Ethernet
-  uint32_t dq_code;     // layer code of Dot1Q
-  bool dq;              // Dot1Q registered
+struct FastCtx {        // wave-uniform facts about the registered set and the options
+  uint32_t mult;        // the fixed-layout hash multiplier
   uint32_t pl_raw;      // Payload as a raw slot: LayerType 2 << 8 | its LUT entry
-  bool cs, hash;        // checksums / flow hashes requested (options)
+  uint32_t unsup;       // status class of a nonzero stop type (IgnoreUnsupported -> OK)
 };
 
-// LE-domain sum of packet bytes [T4, e) where e >= T4 + MINLEN is a runtime end: the words
-// below T4 + MINLEN statically, the rest of the 80 register bytes one word at a time with a
-// select, a ragged last word from LDS, and bytes past 80 in 16-byte LDS chunks.
-template <int T4, int MINLEN, bool SWZ>
-__device__ __forceinline__ uint32_t seg_lesum(const LdsSrc<SWZ> &s, const uint32_t (&h)[20],
-                                              uint32_t e) {
-  constexpr int S = (T4 + MINLEN) & ~3;  // [T4, S) is always inside the segment
-  uint32_t acc = lesum<T4, S>(h, 0u);
-#pragma unroll
-  for (int k = S / 4; k < 20; k++) acc = dot2(e >= 4u * k + 4u ? h[k] : 0u, 0x00010001u, acc);
-  if (__builtin_expect(e & 3u, 0) && e < 80u) {  // ragged end inside the register window
-    const uint32_t x = s.dw(s.pos + (e & ~3u));
-    acc = dot2(__builtin_amdgcn_ubfe(x, 0, 8u * (e & 3u)), 0x00010001u, acc);
-  }
-  if (__builtin_expect(e > 80u, 0)) {
-    uint32_t x = 80;
-    for (; x + 16u <= e; x += 16u) {
-      const uint4 v = s.q(s.pos + x);
-      acc = dot2(v.x, 0x00010001u, acc);
-      acc = dot2(v.y, 0x00010001u, acc);
-      acc = dot2(v.z, 0x00010001u, acc);
-      acc = dot2(v.w, 0x00010001u, acc);
-    }
-    if (x < e) {
-      const uint4 v = s.q(s.pos + x);
-      const uint32_t r = e - x;  // 1..15 bytes
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const uint32_t m = r >= 4u * j + 4u ? w[j]
-                         : (r > 4u * j ? __builtin_amdgcn_ubfe(w[j], 0, 8u * (r - 4u * j)) : 0u);
-        acc = dot2(m, 0x00010001u, acc);
-      }
-    }
-  }
-  return acc;
+// Lookup in a fixed-layout bucket hash (gpd_internal.h kFix*): raw slot, 0x00FF on a miss.
+__device__ __forceinline__ uint32_t fix_bucket_at(uint32_t base, uint32_t mult, uint32_t key) {
+  const uint32_t b = __builtin_amdgcn_ubfe(__umul24(key, mult), 16 - kFixBits, kFixBits);
+  const uint2 v = *reinterpret_cast<const uint2 *>(g_lds + 8 * (base / 2 + b));
+  return (v.x >> 16) == key ? v.x : ((v.y >> 16) == key ? v.y : 0xFFu);
+}
+template <uint32_t BASE>
+__device__ __forceinline__ uint32_t fix_bucket(uint32_t mult, uint32_t key) {
+  return fix_bucket_at(BASE, mult, key);
 }
 
 // TCP/UDP NextLayerType on raw slots (tcp.go:308-314, udp.go:105-110): the dst-port entry
@@ -711,182 +695,204 @@ __device__ __forceinline__ uint32_t ports_next_raw(uint32_t rd, uint32_t rs, uin
   return (rd & 0xFD00u) ? rd : s;
 }
 
-// Transport at compile-time offset T4 with `tl` bytes available (the network payload).
-template <int T4, bool SWZ>
-__device__ __forceinline__ bool fast_tp(const LdsSrc<SWZ> &s, const uint32_t (&h)[20], uint32_t tl,
-                                        uint32_t dec, uint32_t code, const Tab<false> &T,
-                                        const FastCtx &F, Fast &f) {
-  uint32_t next, plen;
-  if (dec == D_TCP) {  // tcp.go:229-314
-    const uint32_t ds = (fbyte<T4 + 12>(h) >> 4) * 4u;
-    if (tl < 20u || ds < 20u || ds > tl) return false;
-    for (uint32_t q = 20; q < ds;) {  // OPTIONS, tcp.go:274-300 (errors -> generic path)
-      const uint32_t k = s.u8(T4 + q);
-      if (k == 0) break;
-      uint32_t ol = 1;
-      if (k != 1) {
-        if (ds - q < 2) return false;
-        ol = s.u8(T4 + q + 1);
-        if (ol < 2 || ol > ds - q) return false;
-      }
-      q += ol;
-    }
-    next = ports_next_raw(T.bucket(T.tcp_base, T.tcp_mult, T.tcp_bits, fbe16<T4 + 2>(h)),
-                          T.bucket(T.tcp_base, T.tcp_mult, T.tcp_bits, fbe16<T4>(h)), F.pl_raw);
-    plen = tl - ds;
-    f.seg_len = tl;
-    if (F.cs) f.seg_sum = seg_lesum<T4, 20>(s, h, T4 + tl);
-  } else {  // UDP, udp.go:30-56
-    const uint32_t length = fbe16<T4 + 4>(h);
-    if (tl < 8u || (length != 0u && length < 8u)) return false;
-    uint32_t hl = tl;
-    if (length >= 8u) {
-      if (length > tl) f.truncated = 1;
-      else hl = length;
-    }
-    next = ports_next_raw(T.bucket(T.udp_base, T.udp_mult, T.udp_bits, fbe16<T4 + 2>(h)),
-                          T.bucket(T.udp_base, T.udp_mult, T.udp_bits, fbe16<T4>(h)), F.pl_raw);
-    plen = hl - 8u;
-    f.seg_len = hl;
-    if (F.cs) f.seg_sum = seg_lesum<T4, 8>(s, h, T4 + hl);
-  }
-  if (F.hash) f.thash = flow_fast(fnv_at<T4, 2>(h), fnv_at<T4 + 2, 2>(h), dec == D_TCP ? 4u : 5u);
-  f.tp = dec == D_TCP ? 1u : 2u;
-  f.codes |= (uint64_t)code << (16 + 4 * f.ncount);
-  f.ncount++;
-  if (plen == 0) return true;
-  const uint32_t nd = next & 15u;
-  if (nd == D_NONE) { f.stop = (next >> 8) & 0xFFu; return true; }
-  if (nd != D_PAYLOAD) return false;  // e.g. VXLAN, a registered app layer
-  f.codes |= (uint64_t)((next >> 4) & 15u) << (16 + 4 * f.ncount);  // Payload consumes the rest
-  f.ncount++;
-  return true;
+// Is this one of the EtherTypes the default tables map to Dot1Q?  Only a guess that lets the
+// network header be fetched early; the table lookup still decides, and a packet whose
+// lookups disagree with the guess goes to the generic decoder.
+__device__ __forceinline__ uint32_t tag_type(uint32_t et) {
+  return (et == 0x8100u || et == 0x88A8u) ? 1u : 0u;
 }
 
-// Network layer at compile-time offset L3; `raw` is the slot Ethernet/Dot1Q looked up.
-template <int L3, bool SWZ>
-__device__ __forceinline__ bool fast_l3(const LdsSrc<SWZ> &s, const uint32_t (&h)[20], uint32_t len,
-                                        uint32_t raw, const Tab<false> &T, const FastCtx &F,
-                                        Fast &f) {
-  const uint32_t dec = raw & 15u;
-  const uint32_t dl = len - L3;
-  uint32_t pv, plen;  // proto-table word of the next header; network payload length
-  if (dec == D_IP4) {  // ip4.go:188-286
-    const uint32_t length = fbe16<L3 + 2>(h);
-    // IHL 5 only (options: generic path); Length 0 (TSO rule) and errors: generic path;
-    // MF or a fragment offset: Fragment, generic path
-    if (dl < 20u || (fbyte<L3>(h) & 0x0Fu) != 5u || length < 20u || (fbe16<L3 + 6>(h) & 0x3FFFu))
-      return false;
-    uint32_t dlen = dl;
-    if (dl > length) dlen = length;
-    else if (dl < length) f.truncated = 1;
-    plen = dlen - 20u;
-    pv = lds_u32(4 * (kHashLutWords + fbyte<L3 + 9>(h)));
-    if (F.cs) {  // checksum(ip4.Contents), ip4.go:158-179; src/dst shared with the pseudo-header
-      f.ps = lesum<L3 + 12, L3 + 20>(h, 0u);
-      f.ipsum = lesum<L3, L3 + 12, L3 + 10>(h, f.ps);
-    }
-    if (F.hash) f.nhash = flow_fast(fnv_at<L3 + 12, 4>(h), fnv_at<L3 + 16, 4>(h), 1u);
-    f.net = 1;
-  } else if (dec == D_IP6) {  // ip6.go:221-278 without hop-by-hop
-    if constexpr (L3 > 18) {
-      return false;  // the transport header would pass the 80-byte register window
-    } else {
-      const uint32_t nh = fbyte<L3 + 6>(h);
-      const uint32_t length = fbe16<L3 + 4>(h);
-      if (dl < 40u || nh == 0u || length == 0u) return false;
-      plen = dl - 40u;
-      if (length > plen) f.truncated = 1;
-      else plen = length;
-      pv = lds_u32(4 * (kHashLutWords + nh));
-      if (F.cs) f.ps = lesum<L3 + 8, L3 + 40>(h, 0u);  // tcpip.go:37-48
-      if (F.hash) {
-        H64 hs = fnv_at<L3 + 8, 4>(h), hd = fnv_at<L3 + 24, 4>(h);
-#pragma unroll  // both chains over the remaining 12 address bytes
-        for (int j = 4; j < 16; j++) {
-          hs.lo ^= (h[(L3 + 8 + j) / 4] >> (8 * ((L3 + 8 + j) % 4))) & 0xFFu;
-          hs = fnv_mulp(hs);
-          hd.lo ^= (h[(L3 + 24 + j) / 4] >> (8 * ((L3 + 24 + j) % 4))) & 0xFFu;
-          hd = fnv_mulp(hd);
-        }
-        f.nhash = flow_fast(hs, hd, 2u);
-      }
-      f.net = 2;
-    }
-  } else {
-    return false;
-  }
-  f.codes |= (uint64_t)((raw >> 4) & 15u) << (16 + 4 * f.ncount);
-  f.ncount++;
-  if (plen == 0) return true;
-  const uint32_t ent = pv >> 16, d2 = ent & 15u;
-  if (d2 == D_NONE) { f.stop = pv & 0xFFFFu; return true; }
-  if (d2 != D_TCP && d2 != D_UDP) return false;
-  if (dec == D_IP4) return fast_tp<L3 + 20>(s, h, plen, d2, ent >> 4, T, F, f);
-  if constexpr (L3 <= 18) return fast_tp<L3 + 40>(s, h, plen, d2, ent >> 4, T, F, f);
-  return false;
-}
-
-template <bool SWZ>
-__device__ __forceinline__ bool fast_decode(const LdsSrc<SWZ> &s, uint32_t len, const Tab<false> &T,
-                                            const FastCtx &F, uint32_t options, Out &o) {
-  if (len < 14) return false;
-  uint32_t h[20];
+// p: LDS address of the packet's first byte; len: its length.  CS / HASH: the fused
+// checksums / flow hashes are requested (GPD_OPT_NO_CHECKSUMS / _NO_FLOW_HASH clear).
+// Three LDS round trips per pass: the Ethernet header; the EtherType lookups together with
+// the 80 bytes from the (guessed) network header on; the protocol and port lookups.
+template <bool CS, bool HASH>
+__device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const FastCtx &F, Out &o) {
+  uint64_t codes = 0;
+  uint32_t nc = 0, trunc = 0, stop = 0;
+  uint32_t ip4 = 0;                  // offset + 1 of the last IPv4 header (0: none)
+  uint32_t net = 0, net_off = 0;     // last network layer (1 v4 / 2 v6) and its offset
+  uint32_t tp = 0, tp_off = 0, tp_len = 0, tp_net = 0, tp_net_off = 0;  // last transport
+  uint32_t b = 0, lim = len;         // this pass's Ethernet offset; end of its data
+  auto put = [&](uint32_t code) { codes |= (uint64_t)code << (16 + 4 * nc); nc++; };
+  for (int pass = 0; pass < 2; pass++) {
+    // Ethernet, ethernet.go:41-62 (802.3 length framing and empty payloads: generic path)
+    if (lim < b + 15u) return false;
+    const U128 e = ld128(p + b + 8);  // bytes 8..23: EtherType and up to two tags
+    const uint32_t et0 = be_lo(e.y), et1 = be_lo(e.z), et2 = be_lo(e.w);
+    if (et0 < 0x0600u) return false;
+    const uint32_t t1 = tag_type(et0), t2 = t1 & tag_type(et1);
+    const uint32_t l3 = b + 14 + 4 * (t1 + t2);
+    uint32_t W[20];  // bytes [l3, l3 + 80)
 #pragma unroll
-  for (int k = 0; k < 5; k++) {
-    const uint4 v = s.q(s.pos + 16 * k);
-    h[4 * k] = v.x; h[4 * k + 1] = v.y; h[4 * k + 2] = v.z; h[4 * k + 3] = v.w;
-  }
-  Fast f{0, 1, 0, 0, 0, (uint64_t)F.eth_code << 16, 0, 0, 0, 0, 0, 0};  // Ethernet, ethernet.go:41-62
-  const uint32_t et = fbe16<12>(h);
-  if (et < 0x0600u) return false;  // 802.3 length framing: generic path
-  uint32_t raw = T.bucket(T.eth_base, T.eth_mult, T.eth_bits, et);
-  bool ok;
-  if (((raw >> 8) & 0xFFu) == GPD_LT_DOT1Q && F.dq) {  // dot1q.go:29-50
-    if (len <= 18) return false;  // short tag or empty Dot1Q payload: generic path
-    f.codes |= (uint64_t)F.dq_code << 20;
-    f.ncount = 2;
-    raw = T.bucket(T.eth_base, T.eth_mult, T.eth_bits, fbe16<16>(h));
-    if (((raw >> 8) & 0xFFu) == GPD_LT_DOT1Q) {
-      if (len <= 22) return false;
-      f.codes |= (uint64_t)F.dq_code << 24;
-      f.ncount = 3;
-      raw = T.bucket(T.eth_base, T.eth_mult, T.eth_bits, fbe16<20>(h));
-      if (((raw >> 8) & 0xFFu) == GPD_LT_DOT1Q) return false;
-      ok = fast_l3<22>(s, h, len, raw, T, F, f);
-    } else {
-      ok = fast_l3<18>(s, h, len, raw, T, F, f);
+    for (int k = 0; k < 5; k++) {
+      const U128 q = ld128(p + l3 + 16 * k);
+      W[4 * k] = q.x; W[4 * k + 1] = q.y; W[4 * k + 2] = q.z; W[4 * k + 3] = q.w;
     }
-  } else {
-    if (len == 14) return false;
-    ok = fast_l3<14>(s, h, len, raw, T, F, f);
+    const uint32_t r0 = fix_bucket<kFixEthBase>(F.mult, et0);
+    uint32_t r1 = 0, r2 = 0;
+    if (t1) {
+      r1 = fix_bucket<kFixEthBase>(F.mult, et1);
+      r2 = fix_bucket<kFixEthBase>(F.mult, et2);
+    }
+    put(GPD_C_ETHERNET);
+    if (((r0 & 15u) == D_DOT1Q) != (t1 != 0)) return false;
+    uint32_t r = r0;
+    if (t1) {  // dot1q.go:29-50, at most two tags here
+      if (lim <= b + 18u) return false;
+      put(GPD_C_DOT1Q);
+      if (((r1 & 15u) == D_DOT1Q) != (t2 != 0)) return false;
+      r = r1;
+      if (t2) {
+        if (lim <= b + 22u || (r2 & 15u) == D_DOT1Q) return false;
+        put(GPD_C_DOT1Q);
+        r = r2;
+      }
+    }
+    const uint32_t dec = r & 15u;
+    if (dec == D_NONE) { stop = (r >> 8) & 0xFFu; break; }
+    const uint32_t dl = lim - l3;
+    uint32_t proto, plen, l4, tx, ty, tw;  // tx..tw: transport bytes 0-3, 4-7, 12-15
+    if (dec == D_IP4) {  // ip4.go:188-286, IHL 5 only
+      const uint32_t length = be_hi(W[0]);
+      // IHL != 5 (options), Length 0 (TSO rule) or < 20 (error), MF / fragment offset
+      // (Fragment): generic path
+      if (dl < 20u || (W[0] & 0x0Fu) != 5u || length < 20u || (be_hi(W[1]) & 0x3FFFu)) return false;
+      uint32_t dlen = dl;
+      if (dl > length) dlen = length;
+      else if (dl < length) trunc = 1;
+      plen = dlen - 20u;
+      proto = (W[2] >> 8) & 0xFFu;
+      ip4 = l3 + 1;
+      net = 1;
+      put(GPD_C_IPV4);
+      lim = l3 + dlen;  // Length trims the payload (and Ethernet padding)
+      l4 = l3 + 20;
+      tx = W[5]; ty = W[6]; tw = W[8];
+    } else if (dec == D_IP6) {  // ip6.go:221-278 without hop-by-hop
+      const uint32_t length = be_lo(W[1]);
+      proto = (W[1] >> 16) & 0xFFu;
+      if (dl < 40u || proto == 0u || length == 0u) return false;
+      plen = dl - 40u;
+      if (length > plen) trunc = 1;
+      else plen = length;
+      net = 2;
+      put(GPD_C_IPV6);
+      lim = l3 + 40 + plen;
+      l4 = l3 + 40;
+      tx = W[10]; ty = W[11]; tw = W[13];
+    } else {
+      return false;
+    }
+    net_off = l3;
+    if (plen == 0) break;
+    // protocol lookup, with the port lookups of the transport the protocol number suggests
+    const uint32_t pv = lds_u32(4 * (kHashLutWords + proto));
+    const uint32_t g = proto == 6u ? 1u : (proto == 17u ? 2u : 0u);
+    uint32_t rd = 0, rs = 0;
+    if (g) {
+      const uint32_t base = g == 1u ? kFixTcpBase : kFixUdpBase;
+      rd = fix_bucket_at(base, F.mult, be_hi(tx));
+      rs = fix_bucket_at(base, F.mult, be_lo(tx));
+    }
+    const uint32_t d4 = (pv >> 16) & 15u;
+    if (d4 == D_NONE) { stop = pv & 0xFFFFu; break; }
+    if (!((d4 == D_TCP && g == 1u) || (d4 == D_UDP && g == 2u))) return false;
+    const uint32_t next = ports_next_raw(rd, rs, F.pl_raw);
+    uint32_t hl, seg;
+    if (d4 == D_TCP) {  // tcp.go:229-314
+      hl = ((tw >> 4) & 15u) * 4u;
+      if (plen < 20u || hl < 20u || hl > plen) return false;
+      for (uint32_t q = 20; q < hl;) {  // OPTIONS, tcp.go:274-300 (errors -> generic path)
+        const uint32_t k = g_lds[p + l4 + q];
+        if (k == 0) break;
+        uint32_t ol = 1;
+        if (k != 1) {
+          if (hl - q < 2) return false;
+          ol = g_lds[p + l4 + q + 1];
+          if (ol < 2 || ol > hl - q) return false;
+        }
+        q += ol;
+      }
+      seg = plen;
+      tp = 1;
+      put(GPD_C_TCP);
+    } else {  // UDP, udp.go:30-56
+      const uint32_t length = be_lo(ty);
+      if (plen < 8u || (length != 0u && length < 8u)) return false;
+      seg = plen;
+      if (length >= 8u) {
+        if (length > plen) trunc = 1;
+        else seg = length;
+      }
+      hl = 8;
+      tp = 2;
+      lim = l4 + seg;
+      put(GPD_C_UDP);
+    }
+    tp_off = l4;
+    tp_len = seg;
+    tp_net = net;
+    tp_net_off = net_off;
+    const uint32_t pl4 = seg - hl;
+    if (pl4 == 0) break;
+    const uint32_t nd = next & 15u;
+    if (nd == D_NONE) { stop = (next >> 8) & 0xFFu; break; }
+    if (nd == D_PAYLOAD) { put(GPD_C_PAYLOAD); break; }  // Payload consumes the rest
+    if (nd != D_VXLAN || pass == 1 || pl4 < 8u) return false;
+    put(GPD_C_VXLAN);  // vxlan.go:53-78; its payload is an Ethernet frame (A11: two passes)
+    b = l4 + hl + 8;
+    if (pl4 == 8u) break;
   }
-  if (!ok) return false;
-  // status / layers / hashes / checksums exactly as decode_packet composes them
-  const uint32_t klass =
-      (f.stop != 0 && !(options & GPD_OPT_IGNORE_UNSUPPORTED)) ? GPD_ST_UNSUPPORTED : GPD_ST_OK;
-  uint32_t st = klass | (f.truncated << 2) | (f.ncount << 4);
+  // outputs, composed exactly as decode_packet does, from the objects' final bytes in LDS
+  uint32_t st = (stop ? F.unsup : GPD_ST_OK) | (trunc << 2) | (nc << 4);
   uint64_t nh = 0, th = 0;
   uint32_t cs = 0;
-  if (F.hash) {
-    nh = f.nhash;
-    st |= (1u << 16) | (f.net << 20);
-    if (f.tp) {
-      th = f.thash;
-      st |= (1u << 17) | ((f.tp == 1 ? 4u : 5u) << 24);
+  if (HASH) {
+    if (net == 1) {  // ip4.NetworkFlow(), ip4.go:63-65
+      const U64 a = ld64(p + net_off + 12);
+      nh = flow_fast(fnv_start<4>(a.x), fnv_start<4>(a.y), 1u);
+    } else {  // ip6.NetworkFlow(), ip6.go:49-51
+      const U128 s = ld128(p + net_off + 8), d = ld128(p + net_off + 24);
+      const H64 hs = fnv_more(fnv_more(fnv_more(fnv_start<4>(s.x), s.y), s.z), s.w);
+      const H64 hd = fnv_more(fnv_more(fnv_more(fnv_start<4>(d.x), d.y), d.z), d.w);
+      nh = flow_fast(hs, hd, 2u);
+    }
+    st |= (1u << 16) | (net << 20);
+    if (tp) {  // TransportFlow(), tcp.go:331-333, udp.go:123-125
+      const uint32_t w = ld32(p + tp_off);
+      th = flow_fast(fnv_start<2>(w), fnv_start<2>(w >> 16), tp == 1 ? 4u : 5u);
+      st |= (1u << 17) | ((tp == 1 ? 4u : 5u) << 24);
     }
   }
-  if (F.cs) {
-    if (f.net == 1) { cs = fold_le_not(f.ipsum); st |= 1u << 18; }
-    if (f.tp) {  // pseudo-header protocol and length as LE-domain words (seg_len < 2^16 here)
-      const uint32_t ps = f.ps + (f.tp == 1 ? 0x0600u : 0x1100u) +
-                          __builtin_amdgcn_perm(0u, f.seg_len, 0x0C0C0001u);
-      cs |= fold_le_not(ps + f.seg_sum) << 16;
+  if (CS) {
+    if (ip4) {  // checksum(ip4.Contents), ip4.go:158-179 (bytes 10-11 left out)
+      const U128 h = ld128(p + ip4 - 1);
+      const uint32_t h4 = ld32(p + ip4 + 15);
+      uint32_t s = dot2(h.x, 0x00010001u, 0u);
+      s = dot2(h.y, 0x00010001u, s);
+      s = dot2(h.z, 0x00000001u, s);
+      s = dot2(h.w, 0x00010001u, s);
+      s = dot2(h4, 0x00010001u, s);
+      cs = fold_le_not(s);
+      st |= 1u << 18;
+    }
+    if (tp) {  // TCP.ComputeChecksum(), tcp.go:193-195 / tcpip.go:26-88
+      uint32_t ps;
+      if (tp_net == 1) {
+        const U64 a = ld64(p + tp_net_off + 12);
+        ps = dot2(a.y, 0x00010001u, dot2(a.x, 0x00010001u, 0u));
+      } else {
+        ps = lesum_lds(p + tp_net_off + 8, 32u, 0u);
+      }
+      // protocol and length as LE-domain words (tp_len < 2^16 in a window)
+      ps += (tp == 1 ? 0x0600u : 0x1100u) + __builtin_amdgcn_perm(0u, tp_len, 0x0C0C0001u);
+      cs |= fold_le_not(lesum_lds(p + tp_off, tp_len, ps)) << 16;
       st |= 1u << 19;
     }
   }
   o.status = st;
-  o.layers = f.codes | (f.stop & 0xFFFFu);
+  o.layers = codes | (stop & 0xFFFFu);
   o.net_hash = nh;
   o.tp_hash = th;
   o.csum = cs;
@@ -950,6 +956,20 @@ __device__ __forceinline__ void glds16(const uint8_t *gbase, uint32_t voff, uint
       : "memory");
 }
 
+// 4-byte LDS-DMA (global_load_lds_dword): lane l's word from gbase + voff lands at LDS lds + 4 l.
+__device__ __forceinline__ void glds4(const void *gbase, uint32_t voff, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dword %1, %2\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(gbase), "s"(lds)
+      : "memory");
+}
+
 // Per-lane source offsets of a window: wave instruction c writes physical slots
 // [64c, 64c+64); lane l's source is the logical slot that lands on slot 64c + l — for the
 // rotated layout that depends on c mod 4 only (four per-lane constants).
@@ -989,8 +1009,18 @@ __device__ __forceinline__ void wait_window(uint32_t nstores) {
 }
 
 // WAVES waves per workgroup; each wave owns 64-packet tiles t, t + W, ... (grid stride).
-template <int STAGE, bool EXT, bool PAGES, bool SWZ, int WAVES>
-__global__ __launch_bounds__(64 * WAVES) void decode_kernel(KParams P) {
+// Per wave, LDS holds two windows (tile k in buffer k & 1) and two descriptor slots (the
+// 64 offsets and 64 caplens of tile k in slot k & 1), all filled by LDS-DMA, so the loop has
+// no compiler-visible global loads and every wait is an explicit, counted one:
+//   iteration k: wait(window k, descriptors k+1) -> plan + issue window k+1 -> issue
+//   descriptors k+2 -> decode tile k from LDS -> result stores.
+// FAST: the straight-line decoder only; a packet it does not take (outside the fast-path
+// envelope, unaligned, larger than a window) is appended to a fallback list that
+// list_kernel decodes with the generic decoder.  Keeping the generic decoder out of this
+// loop keeps its registers out of it too.  !FAST: the generic decoder for every packet.
+template <int STAGE, bool FAST, bool EXT, bool PAGES, bool SWZ, int WAVES, bool CS = true,
+          bool HASH = true>
+__global__ __launch_bounds__(64 * WAVES, 4) void decode_kernel(KParams P) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // stage the dispatch-table image (LUT, ipproto, hashes) into LDS
@@ -1000,72 +1030,72 @@ __global__ __launch_bounds__(64 * WAVES) void decode_kernel(KParams P) {
   const Tab<PAGES> T{P.pages,    P.eth_base, P.tcp_base, P.udp_base, P.eth_bits,
                      P.tcp_bits, P.udp_bits, P.eth_mult, P.tcp_mult, P.udp_mult};
   const uint32_t img = (P.image_words * 4u + 15u) & ~15u;
-  const uint32_t bufs = img + wave * 2u * STAGE;
+  const uint32_t bufs = img + wave * (2u * STAGE + 1024u);
+  const uint32_t dslots = bufs + 2u * STAGE;  // two slots of 64 offsets + 64 caplens
   const uint32_t n = (uint32_t)P.n;  // <= kMaxLaunchPackets per launch
   const uint32_t ntiles = (n + 63u) >> 6;
   const uint32_t nwaves = gridDim.x * WAVES;
   const uint32_t dlen = (uint32_t)P.data_len;
   const uint32_t fits = (uint32_t)STAGE - 15u;  // a packet of <= fits bytes always fits a window
   const uint32_t options = P.options & ~(kDiagSkipDecode | kDiagNoWait);
-  // the fast path assumes Ethernet first (DecodingLayerParser built with LayerTypeEthernet)
-  const bool fast_ok = !PAGES && !EXT && P.first == GPD_LT_ETHERNET &&
-                       (T.lut(GPD_LT_ETHERNET) & 15u) == D_ETH;
-  const FastCtx F{T.lut(GPD_LT_ETHERNET) >> 4, T.lut(GPD_LT_DOT1Q) >> 4,
-                  (T.lut(GPD_LT_DOT1Q) & 15u) == D_DOT1Q,
-                  ((uint32_t)GPD_LT_PAYLOAD << 8) | T.lut(GPD_LT_PAYLOAD),
-                  !(options & GPD_OPT_NO_CHECKSUMS), !(options & GPD_OPT_NO_FLOW_HASH)};
   const DmaLanes<SWZ> L(lane);
-  const Tab<false> &TF = reinterpret_cast<const Tab<false> &>(T);
 
   uint32_t t = blockIdx.x * WAVES + wave;
   if (t >= ntiles) return;
-  // descriptors of tile u (clamped to the buffer at use)
-  auto desc = [&](uint32_t u, uint32_t &off, uint32_t &len) {
-    const uint32_t i = u * 64u + lane;
-    const bool v = u < ntiles && i < n;
-    off = v ? P.offset[i] : 0u;
-    len = v ? P.caplen[i] : 0u;
+  auto desc_issue = [&](uint32_t u, uint32_t slot) {  // descriptors of tile u -> slot
+    if (u < ntiles && u * 64u + lane < n) {
+      glds4(P.offset + u * 64u, 4u * lane, dslots + slot * 512u);
+      glds4(P.caplen + u * 64u, 4u * lane, dslots + slot * 512u + 256u);
+    }
+  };
+  auto desc_read = [&](uint32_t u, uint32_t slot, uint32_t &off, uint32_t &end) {
+    const bool v = u * 64u + lane < n;  // (u < ntiles checked by the caller)
+    const uint32_t o = v ? min(lds_u32(dslots + slot * 512u + 4u * lane), dlen) : 0u;
+    const uint32_t l = v ? min(lds_u32(dslots + slot * 512u + 256u + 4u * lane), dlen - o) : 0u;
+    off = o;  // a packet reaching past data_len is clamped to the buffer
+    end = o + l;
     return v;
   };
-  uint32_t cur = 0;
-  uint32_t off, len;
-  bool valid = desc(t, off, len);
-  off = min(off, dlen);
-  uint32_t end = off + min(len, dlen - off);
+  desc_issue(t, 0);
+  desc_issue(t + nwaves, 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  uint32_t off, end;
+  bool valid = desc_read(t, 0, off, end);
   Window W = plan_window<STAGE>(valid && end - off <= fits, off, end);
   issue_window<SWZ>(P.data, W, bufs, L);
-  uint32_t tn = t + nwaves, off_n, len_n;
-  bool valid_n = desc(tn, off_n, len_n);
+  uint32_t cur = 0;  // buffer / descriptor slot of tile t
+  bool first = true;
 
   for (;;) {
-    // this tile's window and the next tile's descriptors were issued before the last stores
+    // window t and descriptors t + nwaves were issued before the last tile's result stores
     if (!(P.options & kDiagNoWait)) {
-      if (EXT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      else wait_window(P.nstores);
+      if (first || EXT || P.nstores != 5) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
     }
+    first = false;
+    const uint32_t tn = t + nwaves;
     const bool has_next = tn < ntiles;
     Window Wn{0, 0};
-    uint32_t end_n = 0;
+    uint32_t off_n = 0, end_n = 0;
+    bool valid_n = false;
     if (has_next) {  // next tile's first window streams in while this tile decodes
-      off_n = min(off_n, dlen);
-      end_n = off_n + min(len_n, dlen - off_n);
+      valid_n = desc_read(tn, cur ^ 1u, off_n, end_n);
       Wn = plan_window<STAGE>(valid_n && end_n - off_n <= fits, off_n, end_n);
       issue_window<SWZ>(P.data, Wn, bufs + (cur ^ 1u) * STAGE, L);
     }
-    // descriptors two tiles ahead
-    const uint32_t tnn = tn + nwaves;
-    uint32_t off_nn, len_nn;
-    const bool valid_nn = desc(tnn, off_nn, len_nn);
+    desc_issue(tn + nwaves, cur);  // slot `cur` (tile t's) was read one iteration ago
 
     const uint32_t i = t * 64u + lane;
     const uint32_t buf = bufs + cur * STAGE;
     const uint32_t clen = end - off;
-    gpd_ext_rec *ext = EXT && valid ? P.ext + i : nullptr;
-    bool pending = valid;
-    Out o;
-    if (pending && clen > fits) {  // larger than a window: straight from global memory
-      o = decode_packet<EXT>(GlbSrc{P.data, off}, clen, T, P.first, options, ext);
-      store_out(P, i, o);
+    bool pending = valid, fallback = false;
+    if (pending && clen > fits) {  // larger than a window
+      if constexpr (FAST) {
+        fallback = true;
+      } else {  // straight from global memory
+        store_out(P, i, decode_packet<EXT>(GlbSrc{P.data, off}, clen, T, P.first, options,
+                                           EXT ? P.ext + i : nullptr));
+      }
       pending = false;
     }
     bool firstw = true;
@@ -1079,16 +1109,33 @@ __global__ __launch_bounds__(64 * WAVES) void decode_kernel(KParams P) {
       firstw = false;
       const bool in = pending && off >= W.base && end - W.base <= (uint32_t)STAGE;
       if (in && (P.options & kDiagSkipDecode)) {  // diagnostics: data movement only
-        o = Out{g_lds[buf + ((off - W.base) & ~15u)], 0, 0, 0, 0};
-        store_out(P, i, o);
+        store_out(P, i, Out{g_lds[buf + ((off - W.base) & ~15u)], 0, 0, 0, 0});
         pending = false;
       } else if (in) {
         const LdsSrc<SWZ> src{buf, off - W.base};
-        bool done = false;
-        if (fast_ok && (src.pos & 15u) == 0) done = fast_decode<SWZ>(src, clen, TF, F, options, o);
-        if (!done) o = decode_packet<EXT>(src, clen, T, P.first, options, ext);
-        store_out(P, i, o);
+        if constexpr (FAST) {
+          const FastCtx F{P.eth_mult, ((uint32_t)GPD_LT_PAYLOAD << 8) | T.lut(GPD_LT_PAYLOAD),
+                          (options & GPD_OPT_IGNORE_UNSUPPORTED) ? GPD_ST_OK : GPD_ST_UNSUPPORTED};
+          Out o;
+          if (fast_decode<CS, HASH>(src.phys(src.pos), clen, F, o))
+            store_out(P, i, o);
+          else
+            fallback = true;
+        } else {
+          store_out(P, i, decode_packet<EXT>(src, clen, T, P.first, options,
+                                             EXT ? P.ext + i : nullptr));
+        }
         pending = false;
+      }
+    }
+    if constexpr (FAST) {  // append this tile's leftovers to the fallback list
+      const uint64_t m = __ballot(fallback);
+      if (m) {
+        uint32_t base = 0;
+        if (lane == (uint32_t)__builtin_ctzll(m)) base = atomicAdd(P.fb_count, (uint32_t)__popcll(m));
+        base = __builtin_amdgcn_readlane(base, (int)__builtin_ctzll(m));
+        if (fallback) P.fb_list[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = i;
       }
     }
     if (!has_next) break;
@@ -1097,26 +1144,43 @@ __global__ __launch_bounds__(64 * WAVES) void decode_kernel(KParams P) {
     off = off_n;
     end = end_n;
     W = Wn;
-    tn = tnn;
-    valid_n = valid_nn;
-    off_n = off_nn;
-    len_n = len_nn;
     cur ^= 1u;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of the freed buffer / slot done
   }
 }
 
-template <int STAGE, bool EXT, bool PAGES, bool SWZ, int WAVES>
+// The fallback list of the fast kernel: one lane per listed packet, bytes straight from
+// global memory (these packets are rare outside crafted inputs).
+template <bool PAGES>
+__global__ __launch_bounds__(256) void list_kernel(KParams P) {
+  for (uint32_t k = threadIdx.x; k < P.image_words; k += 256)
+    reinterpret_cast<uint32_t *>(g_lds)[k] = P.image[k];
+  __syncthreads();
+  const Tab<PAGES> T{P.pages,    P.eth_base, P.tcp_base, P.udp_base, P.eth_bits,
+                     P.tcp_bits, P.udp_bits, P.eth_mult, P.tcp_mult, P.udp_mult};
+  const uint32_t cnt = *P.fb_count;
+  const uint32_t dlen = (uint32_t)P.data_len;
+  const uint32_t options = P.options & ~(kDiagSkipDecode | kDiagNoWait);
+  for (uint32_t j = blockIdx.x * 256u + threadIdx.x; j < cnt; j += gridDim.x * 256u) {
+    const uint32_t i = P.fb_list[j];
+    const uint32_t off = min(P.offset[i], dlen);
+    const uint32_t len = min(P.caplen[i], dlen - off);
+    store_out(P, i, decode_packet<false>(GlbSrc{P.data, off}, len, T, P.first, options, nullptr));
+  }
+}
+
+template <int STAGE, bool FAST, bool EXT, bool PAGES, bool SWZ, int WAVES, bool CS = true,
+          bool HASH = true>
 static hipError_t launch_t(const KParams &P, hipStream_t stream, int num_cus) {
   const uint64_t ntiles = (P.n + 63) / 64;
   const size_t img = (P.image_words * 4u + 15u) & ~15u;
-  const size_t lds = img + (size_t)STAGE * 2 * WAVES + 320;  // slack: rotated reads past a window end
-  const uint64_t per_cu = (160u * 1024u) / lds;               // resident workgroups per CU (LDS)
+  const size_t lds = img + (size_t)(STAGE * 2 + 1024) * WAVES + 64;  // + slack past the last slot
+  const uint64_t per_cu = (160u * 1024u) / lds;                       // resident workgroups per CU
   uint64_t blocks = (ntiles + WAVES - 1) / WAVES;
   const uint64_t cap = (uint64_t)num_cus * (per_cu ? per_cu : 1) * 4;  // a few tiles per wave
   if (blocks > cap) blocks = cap;
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL((decode_kernel<STAGE, EXT, PAGES, SWZ, WAVES>), dim3((unsigned)blocks),
+  hipLaunchKernelGGL((decode_kernel<STAGE, FAST, EXT, PAGES, SWZ, WAVES, CS, HASH>), dim3((unsigned)blocks),
                      dim3(64 * WAVES), lds, stream, P);
   return hipGetLastError();
 }
@@ -1131,18 +1195,46 @@ static int geom() {
   return g;
 }
 
+// the fast kernel reads headers at any byte address: linear windows
+template <bool CS, bool HASH>
+static hipError_t launch_fast(const KParams &P, hipStream_t stream, int num_cus) {
+  if (P.stage == 4096)
+    return launch_t<4096, true, false, false, false, 4, CS, HASH>(P, stream, num_cus);
+  return launch_t<8192, true, false, false, false, 4, CS, HASH>(P, stream, num_cus);
+}
+
 template <bool EXT, bool PAGES>
 static hipError_t launch_s(const KParams &P, hipStream_t stream, int num_cus) {
   const bool swz = geom() != 1;
   if (P.stage == 4096)
-    return swz ? launch_t<4096, EXT, PAGES, true, 4>(P, stream, num_cus)
-               : launch_t<4096, EXT, PAGES, false, 4>(P, stream, num_cus);
-  return swz ? launch_t<8192, EXT, PAGES, true, 4>(P, stream, num_cus)
-             : launch_t<8192, EXT, PAGES, false, 4>(P, stream, num_cus);
+    return swz ? launch_t<4096, false, EXT, PAGES, true, 4>(P, stream, num_cus)
+               : launch_t<4096, false, EXT, PAGES, false, 4>(P, stream, num_cus);
+  return swz ? launch_t<8192, false, EXT, PAGES, true, 4>(P, stream, num_cus)
+             : launch_t<8192, false, EXT, PAGES, false, 4>(P, stream, num_cus);
+}
+
+bool fast_eligible(const KParams &P) {
+  // the fast kernel: Ethernet first and registered, hashed tables, no extended records
+  return !P.ext && !P.use_pages && P.fixed && P.first == GPD_LT_ETHERNET &&
+         (P.decoders & GPD_DEC_ETHERNET);
 }
 
 hipError_t launch_decode(const KParams &P, hipStream_t stream, int num_cus) {
   if (P.n > kMaxLaunchPackets) return hipErrorInvalidValue;
+  if (fast_eligible(P)) {
+    if (!P.fb_count || !P.fb_list) return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(P.fb_count, 0, sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+    const bool cs = !(P.options & GPD_OPT_NO_CHECKSUMS), hash = !(P.options & GPD_OPT_NO_FLOW_HASH);
+    e = cs ? (hash ? launch_fast<true, true>(P, stream, num_cus)
+                   : launch_fast<true, false>(P, stream, num_cus))
+           : (hash ? launch_fast<false, true>(P, stream, num_cus)
+                   : launch_fast<false, false>(P, stream, num_cus));
+    if (e != hipSuccess) return e;
+    const size_t lds = (P.image_words * 4u + 15u) & ~15u;
+    hipLaunchKernelGGL(list_kernel<false>, dim3((unsigned)num_cus * 2), dim3(256), lds, stream, P);
+    return hipGetLastError();
+  }
   if (P.ext) return P.use_pages ? launch_s<true, true>(P, stream, num_cus)
                                 : launch_s<true, false>(P, stream, num_cus);
   return P.use_pages ? launch_s<false, true>(P, stream, num_cus)
@@ -1159,10 +1251,9 @@ __global__ void probe_fast(KParams P) {
   const Tab<false> T{P.pages,    P.eth_base, P.tcp_base, P.udp_base, P.eth_bits,
                      P.tcp_bits, P.udp_bits, P.eth_mult, P.tcp_mult, P.udp_mult};
   Out o{};
-  const FastCtx F{1, 2, true, 0x2C8, true, true};
-  const bool ok = fast_decode<false>(LdsSrc<false>{0, pos}, len, T, F, P.options, o);
-  const uint32_t i = threadIdx.x;
-  if (ok) store_out(P, i, o);
+  const FastCtx F{P.eth_mult, 0x2C8, 1};
+  (void)T;
+  if (fast_decode<true, true>(pos, len, F, o)) store_out(P, threadIdx.x, o);
 }
 }  // namespace gpd
 #endif

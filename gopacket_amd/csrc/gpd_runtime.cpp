@@ -104,39 +104,73 @@ void type_lut(uint32_t decoders, uint8_t lut[128]) {
 // slots {key << 16 | LayerType << 8 | lut[LayerType]}, bucket = key_hash(key, mult, bits).
 // The multiplier is searched so that no bucket holds more than two keys, which makes every
 // device lookup one ds_read_b64 and two compares (no probe loop).  Unused slots hold a key
-// absent from the table with "LayerType 0, not registered", so they read as a miss.  Usable
-// when every LayerType is < 256 and some (mult, bits) fits max_words; returns false otherwise.
-bool build_hash(const uint16_t *t, const uint8_t lut[128], uint32_t max_words,
-                std::vector<uint32_t> &slots, uint32_t &mult_out, uint32_t &bits_out) {
+// absent from the table with "LayerType 0, not registered", so they read as a miss.
+struct HashKeys {
   std::vector<uint32_t> keys;
+  uint32_t empty = 0;
+  bool ok = false;  // every LayerType < 256 and some key absent
+};
+HashKeys hash_keys(const uint16_t *t) {
+  HashKeys h;
   std::vector<uint8_t> present(65536, 0);
   for (uint32_t k = 0; k < 65536; k++) {
-    if (t[k] >= 256) return false;
-    if (t[k]) { keys.push_back(k); present[k] = 1; }
+    if (t[k] >= 256) return h;
+    if (t[k]) { h.keys.push_back(k); present[k] = 1; }
   }
   uint32_t absent = 0;
   while (absent < 65536 && present[absent]) absent++;
-  if (absent == 65536) return false;
-  const uint32_t empty = (absent << 16) | 0xFFu;
+  if (absent == 65536) return h;
+  h.empty = (absent << 16) | 0xFFu;
+  h.ok = true;
+  return h;
+}
+bool fill_hash(const HashKeys &h, const uint16_t *t, const uint8_t lut[128], uint32_t mult,
+               uint32_t bits, std::vector<uint32_t> &slots) {
+  const uint32_t nb = 1u << bits;
+  if (h.keys.size() > 2 * nb) return false;
+  slots.assign(2 * nb, h.empty);
+  std::vector<uint8_t> fill(nb, 0);
+  for (uint32_t k : h.keys) {
+    const uint32_t b = gpd::key_hash(k, mult, bits);
+    if (fill[b] == 2) return false;
+    slots[2 * b + fill[b]++] = (k << 16) | ((uint32_t)t[k] << 8) | (t[k] < 128 ? lut[t[k]] : 0xFFu);
+  }
+  return true;
+}
+uint32_t next_mult(uint32_t m) { return ((m * 2654435761u + 0x9E37u) & 0xFFFFu) | 1u; }
+
+// Any layout: the smallest bits (<= max_words) with some multiplier.
+bool build_hash(const uint16_t *t, const uint8_t lut[128], uint32_t max_words,
+                std::vector<uint32_t> &slots, uint32_t &mult_out, uint32_t &bits_out) {
+  const HashKeys h = hash_keys(t);
+  if (!h.ok) return false;
   for (uint32_t bits = 2; bits <= 15 && (2u << bits) <= max_words; bits++) {
-    const uint32_t nb = 1u << bits;
-    if (keys.size() > 2 * nb) continue;
     uint32_t mult = 40503u;  // golden-ratio start, then a fixed odd sequence
-    for (int attempt = 0; attempt < 512; attempt++, mult = (mult * 2654435761u + 0x9E37u) & 0xFFFFu) {
-      mult |= 1u;
-      slots.assign(2 * nb, empty);
-      std::vector<uint8_t> fill(nb, 0);
-      bool ok = true;
-      for (uint32_t k : keys) {
-        const uint32_t b = gpd::key_hash(k, mult, bits);
-        if (fill[b] == 2) { ok = false; break; }
-        slots[2 * b + fill[b]++] = (k << 16) | ((uint32_t)t[k] << 8) | (t[k] < 128 ? lut[t[k]] : 0xFFu);
-      }
-      if (ok) {
+    for (int attempt = 0; attempt < 512; attempt++, mult = next_mult(mult)) {
+      if (fill_hash(h, t, lut, mult, bits, slots)) {
         mult_out = mult;
         bits_out = bits;
         return true;
       }
+    }
+  }
+  return false;
+}
+
+// The fixed layout the fast kernel compiles in (gpd_internal.h kFix*): 2^kFixBits buckets
+// per table at fixed bases, one multiplier shared by the three tables.
+bool build_fixed(const uint16_t *eth, const uint16_t *tcp, const uint16_t *udp,
+                 const uint8_t lut[128], std::vector<uint32_t> &he, std::vector<uint32_t> &ht,
+                 std::vector<uint32_t> &hu, uint32_t &mult_out) {
+  const HashKeys ke = hash_keys(eth), kt = hash_keys(tcp), ku = hash_keys(udp);
+  if (!ke.ok || !kt.ok || !ku.ok) return false;
+  uint32_t mult = 40503u;
+  for (int attempt = 0; attempt < 4096; attempt++, mult = next_mult(mult)) {
+    if (fill_hash(ke, eth, lut, mult, gpd::kFixBits, he) &&
+        fill_hash(kt, tcp, lut, mult, gpd::kFixBits, ht) &&
+        fill_hash(ku, udp, lut, mult, gpd::kFixBits, hu)) {
+      mult_out = mult;
+      return true;
     }
   }
   return false;
@@ -155,6 +189,13 @@ struct gpd_ctx {
   uint32_t image_words = 0, use_pages = 0;
   uint32_t eth_base = 0, tcp_base = 0, udp_base = 0, eth_bits = 0, tcp_bits = 0, udp_bits = 0;
   uint32_t eth_mult = 0, tcp_mult = 0, udp_mult = 0;
+  bool fixed = false;  // tables in the fixed layout the fast kernel compiles in
+  // fast-kernel fallback lists, one per stream the context is used on (count + indices)
+  struct Fallback {
+    uint32_t *d = nullptr;
+    uint64_t cap = 0;
+  };
+  std::map<hipStream_t, Fallback> fallback;
   bool timing = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
@@ -206,9 +247,16 @@ int gpd_ctx_reload_tables(gpd_ctx *ctx, const gpd_config *cfg) {
   std::vector<uint32_t> he, ht, hu;
   const uint32_t room = gpd::kHashMaxWords - (uint32_t)img.size();
   uint32_t me = 0, mt = 0, mu = 0, be = 0, bt = 0, bu = 0;
-  const bool hashed = build_hash(eth.data(), lut, room / 2, he, me, be) &&
-                      build_hash(tcp.data(), lut, room / 4, ht, mt, bt) &&
-                      build_hash(udp.data(), lut, room / 4, hu, mu, bu);
+  ctx->fixed = build_fixed(eth.data(), tcp.data(), udp.data(), lut, he, ht, hu, me);
+  bool hashed = ctx->fixed;
+  if (ctx->fixed) {
+    mt = mu = me;
+    be = bt = bu = gpd::kFixBits;
+  } else {
+    hashed = build_hash(eth.data(), lut, room / 2, he, me, be) &&
+             build_hash(tcp.data(), lut, room / 4, ht, mt, bt) &&
+             build_hash(udp.data(), lut, room / 4, hu, mu, bu);
+  }
   HIP_TRY(hipSetDevice(ctx->device));
   if (ctx->d_image) { HIP_TRY(hipFree(ctx->d_image)); ctx->d_image = nullptr; }
   if (ctx->d_pages) { HIP_TRY(hipFree(ctx->d_pages)); ctx->d_pages = nullptr; }
@@ -222,6 +270,9 @@ int gpd_ctx_reload_tables(gpd_ctx *ctx, const gpd_config *cfg) {
     put(he, ctx->eth_base); ctx->eth_bits = be; ctx->eth_mult = me;
     put(ht, ctx->tcp_base); ctx->tcp_bits = bt; ctx->tcp_mult = mt;
     put(hu, ctx->udp_base); ctx->udp_bits = bu; ctx->udp_mult = mu;
+    if (ctx->fixed && (ctx->eth_base != gpd::kFixEthBase || ctx->tcp_base != gpd::kFixTcpBase ||
+                       ctx->udp_base != gpd::kFixUdpBase))
+      return set_err(GPD_ERR_INVALID, "internal: fixed table layout mismatch");
   } else {
     ctx->use_pages = 1;
     std::vector<uint16_t> blob = encode_tables(eth.data(), proto.data(), tcp.data(), udp.data());
@@ -291,6 +342,8 @@ int gpd_ctx_destroy(gpd_ctx *ctx) {
   free_slots(ctx);
   if (ctx->d_image) (void)hipFree(ctx->d_image);
   if (ctx->d_pages) (void)hipFree(ctx->d_pages);
+  for (auto &kv : ctx->fallback)
+    if (kv.second.d) (void)hipFree(kv.second.d);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   delete ctx;
@@ -353,6 +406,7 @@ static int launch(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, hipS
   P.eth_base = ctx->eth_base; P.tcp_base = ctx->tcp_base; P.udp_base = ctx->udp_base;
   P.eth_bits = ctx->eth_bits; P.tcp_bits = ctx->tcp_bits; P.udp_bits = ctx->udp_bits;
   P.eth_mult = ctx->eth_mult; P.tcp_mult = ctx->tcp_mult; P.udp_mult = ctx->udp_mult;
+  P.fixed = ctx->fixed;
   // LDS window per buffer: the smallest of 4/8 KiB that holds a typical 64-packet tile
   const uint64_t mean_slot = (in->data_len + in->n - 1) / in->n;
   P.stage = mean_slot * 64 <= 4096 ? 4096u : 8192u;
@@ -360,6 +414,22 @@ static int launch(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, hipS
   P.decoders = ctx->decoders;
   P.options = ctx->options;
   P.nstores = 2u + (out->net_hash != nullptr) + (out->tp_hash != nullptr) + (out->csum != nullptr);
+  if (gpd::fast_eligible(P)) {  // fallback list scratch for this stream, sized for one launch
+    const uint64_t need = std::min<uint64_t>(in->n, gpd::kMaxLaunchPackets);
+    auto &fb = ctx->fallback[stream];
+    if (fb.cap < need) {
+      if (fb.d) {
+        HIP_TRY(hipStreamSynchronize(stream));
+        HIP_TRY(hipFree(fb.d));
+        fb.d = nullptr;
+        fb.cap = 0;
+      }
+      HIP_TRY(hipMalloc(&fb.d, (need + 64) * sizeof(uint32_t)));
+      fb.cap = need;
+    }
+    P.fb_count = fb.d;
+    P.fb_list = fb.d + 64;  // count in its own 256-byte line
+  }
   if (record) HIP_TRY(hipEventRecord(ctx->ev0, stream));
   // launches of <= kMaxLaunchPackets packets keep every packet/tile index 32-bit in the kernel
   for (uint64_t lo = 0; lo < in->n; lo += gpd::kMaxLaunchPackets) {
