@@ -40,6 +40,9 @@ namespace gpd {
 
 constexpr uint32_t kDiagSkipDecode = 1u << 31;  // internal diagnostic option (bench --ablate nodecode)
 constexpr uint32_t kDiagNoWait = 1u << 30;      // internal diagnostic: skip the per-tile DMA wait
+constexpr uint32_t kDiagNtLoad = 1u << 29;      // A/B: window LDS-DMA with the nt cache policy
+constexpr uint32_t kDiagNtStore = 1u << 28;     // A/B: result stores with the nt cache policy
+constexpr uint32_t kDiagMask = kDiagSkipDecode | kDiagNoWait | kDiagNtLoad | kDiagNtStore;
 
 extern __shared__ __attribute__((aligned(16))) uint8_t g_lds[];
 
@@ -645,6 +648,7 @@ constexpr uint64_t kFnvC0 = (kFnvBasis & ~0xFFull) * kFnvPrime;  // (basis with 
 // fnvHash of the NB low bytes of w (byte 0 first), from the basis
 template <int NB>
 __device__ __forceinline__ H64 fnv_start(uint32_t w) {
+  static_assert(NB == 2 || NB == 4, "fnv_start<2|4>");
   // byte 0 in closed form: (basis ^ b) * prime = C0 + c * 0x1b3 + (c << 40), c = b ^ 0x25
   const uint32_t c = (w & 0xFFu) ^ (uint32_t)(kFnvBasis & 0xFFu);
   const uint64_t r = (uint64_t)c * 0x1b3u + kFnvC0;
@@ -697,48 +701,80 @@ __device__ __forceinline__ uint32_t ports_next_raw(uint32_t rd, uint32_t rs, uin
 
 // Is this one of the EtherTypes the default tables map to Dot1Q?  Only a guess that lets the
 // network header be fetched early; the table lookup still decides, and a packet whose
-// lookups disagree with the guess goes to the generic decoder.
+// lookups disagree with a guess goes to the generic decoder.
 __device__ __forceinline__ uint32_t tag_type(uint32_t et) {
   return (et == 0x8100u || et == 0x88A8u) ? 1u : 0u;
 }
 
+__device__ __forceinline__ void load80(uint32_t (&W)[20], uint32_t a) {
+#pragma unroll
+  for (int k = 0; k < 5; k++) {
+    const U128 q = ld128(a + 16 * k);
+    W[4 * k] = q.x; W[4 * k + 1] = q.y; W[4 * k + 2] = q.z; W[4 * k + 3] = q.w;
+  }
+}
+
 // p: LDS address of the packet's first byte; len: its length.  CS / HASH: the fused
 // checksums / flow hashes are requested (GPD_OPT_NO_CHECKSUMS / _NO_FLOW_HASH clear).
-// Three LDS round trips per pass: the Ethernet header; the EtherType lookups together with
-// the 80 bytes from the (guessed) network header on; the protocol and port lookups.
+// Two dependent LDS round trips per pass (three for tagged frames): (1) the Ethernet header
+// and the 80 bytes after it; (2) every table lookup — EtherType, protocol, ports, each on
+// a guess read from the bytes (IPv4/IPv6 by the version nibble, TCP/UDP by the protocol
+// number) — together with the transport segment's first and last 16-byte chunks.  The
+// lookups then confirm the guesses; a packet they contradict goes to the generic decoder.
+// Hashes and checksums are computed from registers as each layer is accepted, so VXLAN's
+// second pass overwrites them exactly as the reused layer objects are overwritten (A11).
 template <bool CS, bool HASH>
 __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const FastCtx &F, Out &o) {
-  uint64_t codes = 0;
+  uint64_t codes = 0, nh = 0, th = 0;
   uint32_t nc = 0, trunc = 0, stop = 0;
-  uint32_t ip4 = 0;                  // offset + 1 of the last IPv4 header (0: none)
-  uint32_t net = 0, net_off = 0;     // last network layer (1 v4 / 2 v6) and its offset
-  uint32_t tp = 0, tp_off = 0, tp_len = 0, tp_net = 0, tp_net_off = 0;  // last transport
-  uint32_t b = 0, lim = len;         // this pass's Ethernet offset; end of its data
+  uint32_t net = 0, tp = 0, ip4 = 0, ipcs = 0;
+  uint32_t tp_off = 0, tp_len = 0, tp_ps = 0;  // the last transport and its pseudo-header sum
+  U128 c0{0, 0, 0, 0}, ct{0, 0, 0, 0};        // its segment's first / ragged-last chunk
+  uint32_t b = 0, lim = len;                   // this pass's Ethernet offset; end of its data
   auto put = [&](uint32_t code) { codes |= (uint64_t)code << (16 + 4 * nc); nc++; };
   for (int pass = 0; pass < 2; pass++) {
-    // Ethernet, ethernet.go:41-62 (802.3 length framing and empty payloads: generic path)
-    if (lim < b + 15u) return false;
+    // ---- round trip 1: Ethernet header (ethernet.go:41-62) and the bytes after it
+    if (lim < b + 15u) return false;  // too small, or an empty payload: generic path
     const U128 e = ld128(p + b + 8);  // bytes 8..23: EtherType and up to two tags
+    uint32_t W[20];
+    load80(W, p + b + 14);
     const uint32_t et0 = be_lo(e.y), et1 = be_lo(e.z), et2 = be_lo(e.w);
-    if (et0 < 0x0600u) return false;
+    if (et0 < 0x0600u) return false;  // 802.3 length framing
     const uint32_t t1 = tag_type(et0), t2 = t1 & tag_type(et1);
     const uint32_t l3 = b + 14 + 4 * (t1 + t2);
-    uint32_t W[20];  // bytes [l3, l3 + 80)
-#pragma unroll
-    for (int k = 0; k < 5; k++) {
-      const U128 q = ld128(p + l3 + 16 * k);
-      W[4 * k] = q.x; W[4 * k + 1] = q.y; W[4 * k + 2] = q.z; W[4 * k + 3] = q.w;
-    }
+    if (t1) load80(W, p + l3);  // tagged: the network header is further in
+    // ---- guesses from the bytes
+    const uint32_t ver = (W[0] >> 4) & 15u;
+    const bool v4 = ver == 4u;
+    const uint32_t proto = v4 ? ((W[2] >> 8) & 0xFFu) : ((W[1] >> 16) & 0xFFu);
+    const uint32_t g = proto == 6u ? 1u : (proto == 17u ? 2u : 0u);  // TCP / UDP
+    const uint32_t tx = v4 ? W[5] : W[10], ty = v4 ? W[6] : W[11], tw = v4 ? W[8] : W[13];
+    const uint32_t l4 = l3 + (v4 ? 20u : 40u);
+    const uint32_t dl = lim - l3;
+    const uint32_t length = v4 ? be_hi(W[0]) : be_lo(W[1]);  // IPv4 total / IPv6 payload
+    uint32_t plen;                                             // the network payload
+    if (v4) plen = (dl > length ? length : dl) - 20u;
+    else plen = (length > dl - 40u) ? dl - 40u : length;
+    const uint32_t ulen = be_lo(ty);
+    const uint32_t seg = (g == 2u && ulen >= 8u && ulen <= plen) ? ulen : plen;
+    const uint32_t xt = (seg < 16384u ? seg : 0u) & ~15u;  // (a guess: keep it in the window)
+    // ---- round trip 2: all lookups, and the segment chunks
     const uint32_t r0 = fix_bucket<kFixEthBase>(F.mult, et0);
     uint32_t r1 = 0, r2 = 0;
     if (t1) {
       r1 = fix_bucket<kFixEthBase>(F.mult, et1);
       r2 = fix_bucket<kFixEthBase>(F.mult, et2);
     }
+    const uint32_t pv = lds_u32(4 * (kHashLutWords + proto));
+    const uint32_t pbase = g == 1u ? kFixTcpBase : kFixUdpBase;
+    const uint32_t rd = fix_bucket_at(pbase, F.mult, be_hi(tx));
+    const uint32_t rs = fix_bucket_at(pbase, F.mult, be_lo(tx));
+    const U128 n0 = ld128(p + l4), nt = ld128(p + l4 + xt);
+    // ---- Ethernet / Dot1Q (dot1q.go:29-50), confirming the tag guesses
     put(GPD_C_ETHERNET);
     if (((r0 & 15u) == D_DOT1Q) != (t1 != 0)) return false;
     uint32_t r = r0;
-    if (t1) {  // dot1q.go:29-50, at most two tags here
+    if (t1) {
       if (lim <= b + 18u) return false;
       put(GPD_C_DOT1Q);
       if (((r1 & 15u) == D_DOT1Q) != (t2 != 0)) return false;
@@ -751,56 +787,47 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
     }
     const uint32_t dec = r & 15u;
     if (dec == D_NONE) { stop = (r >> 8) & 0xFFu; break; }
-    const uint32_t dl = lim - l3;
-    uint32_t proto, plen, l4, tx, ty, tw;  // tx..tw: transport bytes 0-3, 4-7, 12-15
+    uint32_t ps;  // pseudo-header address words of this network layer (LE domain)
     if (dec == D_IP4) {  // ip4.go:188-286, IHL 5 only
-      const uint32_t length = be_hi(W[0]);
       // IHL != 5 (options), Length 0 (TSO rule) or < 20 (error), MF / fragment offset
       // (Fragment): generic path
-      if (dl < 20u || (W[0] & 0x0Fu) != 5u || length < 20u || (be_hi(W[1]) & 0x3FFFu)) return false;
-      uint32_t dlen = dl;
-      if (dl > length) dlen = length;
-      else if (dl < length) trunc = 1;
-      plen = dlen - 20u;
-      proto = (W[2] >> 8) & 0xFFu;
-      ip4 = l3 + 1;
+      if (!v4 || dl < 20u || (W[0] & 0x0Fu) != 5u || length < 20u || (be_hi(W[1]) & 0x3FFFu))
+        return false;
+      if (dl < length) trunc = 1;
+      ps = dot2(W[4], 0x00010001u, dot2(W[3], 0x00010001u, 0u));
+      if (CS) {  // checksum(ip4.Contents), ip4.go:158-179 (bytes 10-11 left out)
+        ipcs = fold_le_not(dot2(W[2], 0x00000001u, dot2(W[1], 0x00010001u,
+                           dot2(W[0], 0x00010001u, ps))));
+        ip4 = 1;
+      }
+      if (HASH) nh = flow_fast(fnv_start<4>(W[3]), fnv_start<4>(W[4]), 1u);  // ip4.go:63-65
       net = 1;
       put(GPD_C_IPV4);
-      lim = l3 + dlen;  // Length trims the payload (and Ethernet padding)
-      l4 = l3 + 20;
-      tx = W[5]; ty = W[6]; tw = W[8];
+      lim = l3 + 20u + plen;  // Length trims the payload (and Ethernet padding)
     } else if (dec == D_IP6) {  // ip6.go:221-278 without hop-by-hop
-      const uint32_t length = be_lo(W[1]);
-      proto = (W[1] >> 16) & 0xFFu;
-      if (dl < 40u || proto == 0u || length == 0u) return false;
-      plen = dl - 40u;
-      if (length > plen) trunc = 1;
-      else plen = length;
+      if (ver != 6u || dl < 40u || proto == 0u || length == 0u) return false;
+      if (length > dl - 40u) trunc = 1;
+      ps = 0;
+#pragma unroll
+      for (int k = 2; k < 10; k++) ps = dot2(W[k], 0x00010001u, ps);  // tcpip.go:37-48
+      if (HASH) {  // ip6.go:49-51
+        const H64 hs = fnv_more(fnv_more(fnv_more(fnv_start<4>(W[2]), W[3]), W[4]), W[5]);
+        const H64 hd = fnv_more(fnv_more(fnv_more(fnv_start<4>(W[6]), W[7]), W[8]), W[9]);
+        nh = flow_fast(hs, hd, 2u);
+      }
       net = 2;
       put(GPD_C_IPV6);
-      lim = l3 + 40 + plen;
-      l4 = l3 + 40;
-      tx = W[10]; ty = W[11]; tw = W[13];
+      lim = l3 + 40u + plen;
     } else {
       return false;
     }
-    net_off = l3;
     if (plen == 0) break;
-    // protocol lookup, with the port lookups of the transport the protocol number suggests
-    const uint32_t pv = lds_u32(4 * (kHashLutWords + proto));
-    const uint32_t g = proto == 6u ? 1u : (proto == 17u ? 2u : 0u);
-    uint32_t rd = 0, rs = 0;
-    if (g) {
-      const uint32_t base = g == 1u ? kFixTcpBase : kFixUdpBase;
-      rd = fix_bucket_at(base, F.mult, be_hi(tx));
-      rs = fix_bucket_at(base, F.mult, be_lo(tx));
-    }
+    // ---- transport, confirming the protocol guess
     const uint32_t d4 = (pv >> 16) & 15u;
     if (d4 == D_NONE) { stop = pv & 0xFFFFu; break; }
     if (!((d4 == D_TCP && g == 1u) || (d4 == D_UDP && g == 2u))) return false;
-    const uint32_t next = ports_next_raw(rd, rs, F.pl_raw);
-    uint32_t hl, seg;
-    if (d4 == D_TCP) {  // tcp.go:229-314
+    uint32_t hl;
+    if (g == 1u) {  // tcp.go:229-314
       hl = ((tw >> 4) & 15u) * 4u;
       if (plen < 20u || hl < 20u || hl > plen) return false;
       for (uint32_t q = 20; q < hl;) {  // OPTIONS, tcp.go:274-300 (errors -> generic path)
@@ -814,29 +841,25 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
         }
         q += ol;
       }
-      seg = plen;
-      tp = 1;
       put(GPD_C_TCP);
-    } else {  // UDP, udp.go:30-56
-      const uint32_t length = be_lo(ty);
-      if (plen < 8u || (length != 0u && length < 8u)) return false;
-      seg = plen;
-      if (length >= 8u) {
-        if (length > plen) trunc = 1;
-        else seg = length;
-      }
+    } else {  // UDP, udp.go:30-56 (Length 0: the rest; 1..7: error)
+      if (plen < 8u || (ulen != 0u && ulen < 8u)) return false;
+      if (ulen > plen) trunc = 1;
       hl = 8;
-      tp = 2;
       lim = l4 + seg;
       put(GPD_C_UDP);
     }
+    tp = g;
+    if (HASH) th = flow_fast(fnv_start<2>(tx), fnv_start<2>(tx >> 16), g == 1u ? 4u : 5u);
+    // pseudo-header protocol and length as LE-domain words (seg < 2^16 in a window)
+    tp_ps = ps + (g == 1u ? 0x0600u : 0x1100u) + __builtin_amdgcn_perm(0u, seg, 0x0C0C0001u);
     tp_off = l4;
     tp_len = seg;
-    tp_net = net;
-    tp_net_off = net_off;
+    c0 = n0;
+    ct = nt;
     const uint32_t pl4 = seg - hl;
     if (pl4 == 0) break;
-    const uint32_t nd = next & 15u;
+    const uint32_t next = ports_next_raw(rd, rs, F.pl_raw), nd = next & 15u;
     if (nd == D_NONE) { stop = (next >> 8) & 0xFFu; break; }
     if (nd == D_PAYLOAD) { put(GPD_C_PAYLOAD); break; }  // Payload consumes the rest
     if (nd != D_VXLAN || pass == 1 || pl4 < 8u) return false;
@@ -844,57 +867,45 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
     b = l4 + hl + 8;
     if (pl4 == 8u) break;
   }
-  // outputs, composed exactly as decode_packet does, from the objects' final bytes in LDS
+  // ---- outputs, composed exactly as decode_packet does
   uint32_t st = (stop ? F.unsup : GPD_ST_OK) | (trunc << 2) | (nc << 4);
-  uint64_t nh = 0, th = 0;
   uint32_t cs = 0;
   if (HASH) {
-    if (net == 1) {  // ip4.NetworkFlow(), ip4.go:63-65
-      const U64 a = ld64(p + net_off + 12);
-      nh = flow_fast(fnv_start<4>(a.x), fnv_start<4>(a.y), 1u);
-    } else {  // ip6.NetworkFlow(), ip6.go:49-51
-      const U128 s = ld128(p + net_off + 8), d = ld128(p + net_off + 24);
-      const H64 hs = fnv_more(fnv_more(fnv_more(fnv_start<4>(s.x), s.y), s.z), s.w);
-      const H64 hd = fnv_more(fnv_more(fnv_more(fnv_start<4>(d.x), d.y), d.z), d.w);
-      nh = flow_fast(hs, hd, 2u);
-    }
-    st |= (1u << 16) | (net << 20);
-    if (tp) {  // TransportFlow(), tcp.go:331-333, udp.go:123-125
-      const uint32_t w = ld32(p + tp_off);
-      th = flow_fast(fnv_start<2>(w), fnv_start<2>(w >> 16), tp == 1 ? 4u : 5u);
-      st |= (1u << 17) | ((tp == 1 ? 4u : 5u) << 24);
-    }
+    st |= (1u << 16) | (net << 20) | (tp ? (1u << 17) | ((tp == 1 ? 4u : 5u) << 24) : 0u);
   }
   if (CS) {
-    if (ip4) {  // checksum(ip4.Contents), ip4.go:158-179 (bytes 10-11 left out)
-      const U128 h = ld128(p + ip4 - 1);
-      const uint32_t h4 = ld32(p + ip4 + 15);
-      uint32_t s = dot2(h.x, 0x00010001u, 0u);
-      s = dot2(h.y, 0x00010001u, s);
-      s = dot2(h.z, 0x00000001u, s);
-      s = dot2(h.w, 0x00010001u, s);
-      s = dot2(h4, 0x00010001u, s);
-      cs = fold_le_not(s);
-      st |= 1u << 18;
+    // TCP.ComputeChecksum(), tcp.go:193-195 / tcpip.go:52-88 over the last transport
+    uint32_t s = tp_ps;
+    const uint32_t w0 = tp_len >= 16u ? 0x00010001u : 0u;  // first whole chunk
+    s = dot2(c0.x, w0, s);
+    s = dot2(c0.y, w0, s);
+    s = dot2(c0.z, w0, s);
+    s = dot2(c0.w, w0, s);
+    // ragged tail: the first tp_len % 16 bytes of ct (an odd last byte is the low byte of
+    // its half)
+    const uint32_t r8 = (tp_len & 15u) * 8u;
+    uint64_t lo = ((uint64_t)ct.y << 32) | ct.x, hi = ((uint64_t)ct.w << 32) | ct.z;
+    lo = r8 >= 64u ? lo : (r8 ? (lo << (64u - r8)) >> (64u - r8) : 0ull);
+    hi = r8 > 64u ? (hi << (128u - r8)) >> (128u - r8) : 0ull;
+    s = dot2((uint32_t)lo, 0x00010001u, s);
+    s = dot2((uint32_t)(lo >> 32), 0x00010001u, s);
+    s = dot2((uint32_t)hi, 0x00010001u, s);
+    s = dot2((uint32_t)(hi >> 32), 0x00010001u, s);
+    const uint32_t xt = tp_len & ~15u;
+    for (uint32_t x = 16; x < xt; x += 16u) {  // whole chunks after the first (long segments)
+      const U128 q = ld128(p + tp_off + x);
+      s = dot2(q.x, 0x00010001u, s);
+      s = dot2(q.y, 0x00010001u, s);
+      s = dot2(q.z, 0x00010001u, s);
+      s = dot2(q.w, 0x00010001u, s);
     }
-    if (tp) {  // TCP.ComputeChecksum(), tcp.go:193-195 / tcpip.go:26-88
-      uint32_t ps;
-      if (tp_net == 1) {
-        const U64 a = ld64(p + tp_net_off + 12);
-        ps = dot2(a.y, 0x00010001u, dot2(a.x, 0x00010001u, 0u));
-      } else {
-        ps = lesum_lds(p + tp_net_off + 8, 32u, 0u);
-      }
-      // protocol and length as LE-domain words (tp_len < 2^16 in a window)
-      ps += (tp == 1 ? 0x0600u : 0x1100u) + __builtin_amdgcn_perm(0u, tp_len, 0x0C0C0001u);
-      cs |= fold_le_not(lesum_lds(p + tp_off, tp_len, ps)) << 16;
-      st |= 1u << 19;
-    }
+    cs = (ip4 ? ipcs : 0u) | (tp ? fold_le_not(s) << 16 : 0u);
+    st |= (ip4 ? 1u << 18 : 0u) | (tp ? 1u << 19 : 0u);
   }
   o.status = st;
   o.layers = codes | (stop & 0xFFFFu);
-  o.net_hash = nh;
-  o.tp_hash = th;
+  o.net_hash = HASH ? nh : 0;
+  o.tp_hash = HASH ? th : 0;
   o.csum = cs;
   return true;
 }
@@ -907,6 +918,14 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 }
 
 __device__ __forceinline__ void store_out(const KParams &P, uint32_t i, const Out &o) {
+  if (P.options & kDiagNtStore) {
+    __builtin_nontemporal_store(o.status, P.status + i);
+    __builtin_nontemporal_store(o.layers, P.layers + i);
+    if (P.net_hash) __builtin_nontemporal_store(o.net_hash, P.net_hash + i);
+    if (P.tp_hash) __builtin_nontemporal_store(o.tp_hash, P.tp_hash + i);
+    if (P.csum) __builtin_nontemporal_store(o.csum, P.csum + i);
+    return;
+  }
   P.status[i] = o.status;
   P.layers[i] = o.layers;
   if (P.net_hash) P.net_hash[i] = o.net_hash;
@@ -943,8 +962,21 @@ __device__ __forceinline__ Window plan_window(bool pending, uint32_t off, uint32
 // ds_reads and drains it (vmcnt(0)) before the first one, serialising the prefetch.  Every
 // wait on these loads is therefore explicit (a counted s_waitcnt vmcnt before a window is
 // read; loads, stores and LDS-DMA retire in issue order, MI355X_MICROARCH.md).
-__device__ __forceinline__ void glds16(const uint8_t *gbase, uint32_t voff, uint32_t lds) {
+__device__ __forceinline__ void glds16(const uint8_t *gbase, uint32_t voff, uint32_t lds,
+                                       bool nt = false) {
   uint32_t keep;
+  if (nt) {
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %3\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, %2 nt\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(gbase), "s"(lds)
+        : "memory");
+    return;
+  }
   asm volatile(
       "s_mov_b32 %0, m0\n\t"
       "s_mov_b32 m0, %3\n\t"
@@ -985,13 +1017,14 @@ struct DmaLanes {
 
 template <bool SWZ>
 __device__ __forceinline__ void issue_window(const uint8_t *data, const Window &w, uint32_t buf,
-                                             const DmaLanes<SWZ> &L) {
+                                             const DmaLanes<SWZ> &L, bool nt = false) {
   for (uint32_t c4 = 0; c4 < w.nbytes; c4 += 4096u) {
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       const uint32_t c = c4 + 1024u * j;
       if (c >= w.nbytes) break;
-      if (c + 1024u <= w.nbytes || c + L.voff[j] < w.nbytes) glds16(data + w.base + c, L.voff[j], buf + c);
+      if (c + 1024u <= w.nbytes || c + L.voff[j] < w.nbytes)
+        glds16(data + w.base + c, L.voff[j], buf + c, nt);
     }
   }
 }
@@ -1008,19 +1041,23 @@ __device__ __forceinline__ void wait_window(uint32_t nstores) {
   }
 }
 
-// WAVES waves per workgroup; each wave owns 64-packet tiles t, t + W, ... (grid stride).
-// Per wave, LDS holds two windows (tile k in buffer k & 1) and two descriptor slots (the
-// 64 offsets and 64 caplens of tile k in slot k & 1), all filled by LDS-DMA, so the loop has
-// no compiler-visible global loads and every wait is an explicit, counted one:
-//   iteration k: wait(window k, descriptors k+1) -> plan + issue window k+1 -> issue
-//   descriptors k+2 -> decode tile k from LDS -> result stores.
+// WAVES waves per workgroup; each wave owns 64-packet tiles t, t + W, ... (grid stride).  A
+// tile's bytes are staged through LDS windows of STAGE bytes (a tile of large packets takes
+// several), and the window is the pipeline unit: per wave, LDS holds two window buffers
+// and two descriptor slots (the 64 offsets and caplens of a tile), all filled by LDS-DMA,
+// so the loop has no compiler-visible global loads and every wait is an explicit, counted
+// one.  Iteration k:
+//   wait for window k -> plan and issue window k+1 (the rest of this tile, or the next
+//   tile's first window, whose descriptors arrived two tiles ago; then the descriptors two
+//   tiles further on) -> decode window k's packets from LDS -> when window k ended its
+//   tile, store the tile's 64 results.
 // FAST: the straight-line decoder only; a packet it does not take (outside the fast-path
-// envelope, unaligned, larger than a window) is appended to a fallback list that
-// list_kernel decodes with the generic decoder.  Keeping the generic decoder out of this
-// loop keeps its registers out of it too.  !FAST: the generic decoder for every packet.
+// envelope, larger than a window) goes to a fallback list that list_kernel decodes with the
+// generic decoder.  Keeping the generic decoder out of this loop keeps its registers out of
+// it too.  !FAST: the generic decoder for every packet.
 template <int STAGE, bool FAST, bool EXT, bool PAGES, bool SWZ, int WAVES, bool CS = true,
-          bool HASH = true>
-__global__ __launch_bounds__(64 * WAVES, 4) void decode_kernel(KParams P) {
+          bool HASH = true, int MINW = 1>
+__global__ __launch_bounds__(64 * WAVES, MINW) void decode_kernel(KParams P) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // stage the dispatch-table image (LUT, ipproto, hashes) into LDS
@@ -1037,115 +1074,148 @@ __global__ __launch_bounds__(64 * WAVES, 4) void decode_kernel(KParams P) {
   const uint32_t nwaves = gridDim.x * WAVES;
   const uint32_t dlen = (uint32_t)P.data_len;
   const uint32_t fits = (uint32_t)STAGE - 15u;  // a packet of <= fits bytes always fits a window
-  const uint32_t options = P.options & ~(kDiagSkipDecode | kDiagNoWait);
+  const uint32_t options = P.options & ~kDiagMask;
+  const bool nt = P.options & kDiagNtLoad;
+  const uint32_t nst = EXT ? 0u : P.nstores;  // result stores per tile (EXT: drain fully)
   const DmaLanes<SWZ> L(lane);
 
-  uint32_t t = blockIdx.x * WAVES + wave;
-  if (t >= ntiles) return;
-  auto desc_issue = [&](uint32_t u, uint32_t slot) {  // descriptors of tile u -> slot
-    if (u < ntiles && u * 64u + lane < n) {
+  uint32_t tp = blockIdx.x * WAVES + wave;  // the planner's tile
+  if (tp >= ntiles) return;
+  auto desc_issue = [&](uint32_t u, uint32_t slot) -> uint32_t {  // descriptors of tile u
+    if (u >= ntiles) return 0u;
+    if (u * 64u + lane < n) {
       glds4(P.offset + u * 64u, 4u * lane, dslots + slot * 512u);
       glds4(P.caplen + u * 64u, 4u * lane, dslots + slot * 512u + 256u);
     }
+    return 2u;  // VMEM instructions issued
   };
-  auto desc_read = [&](uint32_t u, uint32_t slot, uint32_t &off, uint32_t &end) {
-    const bool v = u * 64u + lane < n;  // (u < ntiles checked by the caller)
+  // per-lane flags are kept as 0/1 words (VGPRs), not lane masks (SGPR pairs)
+  auto desc_read = [&](uint32_t u, uint32_t slot, uint32_t &off, uint32_t &end) -> uint32_t {
+    const uint32_t v = u * 64u + lane < n ? 1u : 0u;
     const uint32_t o = v ? min(lds_u32(dslots + slot * 512u + 4u * lane), dlen) : 0u;
     const uint32_t l = v ? min(lds_u32(dslots + slot * 512u + 256u + 4u * lane), dlen - o) : 0u;
     off = o;  // a packet reaching past data_len is clamped to the buffer
     end = o + l;
     return v;
   };
-  desc_issue(t, 0);
-  desc_issue(t + nwaves, 1);
+  auto covered = [&](const Window &w, uint32_t pend, uint32_t off, uint32_t end) -> uint32_t {
+    return (pend && off >= w.base && end - w.base <= (uint32_t)STAGE) ? 1u : 0u;
+  };
+
+  // prologue: descriptors of the first two tiles, then the first window
+  desc_issue(tp, 0);
+  desc_issue(tp + nwaves, 1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  uint32_t off, end;
-  bool valid = desc_read(t, 0, off, end);
-  Window W = plan_window<STAGE>(valid && end - off <= fits, off, end);
-  issue_window<SWZ>(P.data, W, bufs, L);
-  uint32_t cur = 0;  // buffer / descriptor slot of tile t
-  bool first = true;
+  uint32_t slot = 0;  // descriptor slot of the planner's tile
+  uint32_t off_p, end_p;
+  uint32_t valid_p = desc_read(tp, slot, off_p, end_p);
+  uint32_t pend_p = (valid_p && end_p - off_p <= fits) ? 1u : 0u;  // still to be given a window
+  const uint32_t big0 = valid_p & (pend_p ^ 1u);
+  Window Wd = plan_window<STAGE>(pend_p != 0, off_p, end_p);
+  uint32_t cov_d = covered(Wd, pend_p, off_p, end_p);
+  pend_p &= cov_d ^ 1u;
+  issue_window<SWZ>(P.data, Wd, bufs, L, nt);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read before it is restaged
+  uint32_t nwait = desc_issue(tp + 2u * nwaves, slot);
 
+  // decode state: the window in flight belongs to tile td
+  uint32_t td = tp, off_d = off_p, end_d = end_p;
+  uint32_t valid_d = valid_p, big_d = big0;
+  bool first_d = true;
+  uint32_t cur = 0;  // buffer of the window to decode
+  Out res{0, 0, 0, 0, 0};
+  uint32_t fb = 0;
   for (;;) {
-    // window t and descriptors t + nwaves were issued before the last tile's result stores
+    // window cur landed: wait for all but the VMEM instructions issued after it
     if (!(P.options & kDiagNoWait)) {
-      if (first || EXT || P.nstores != 5) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      switch (nwait) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+        case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+      }
     }
-    first = false;
-    const uint32_t tn = t + nwaves;
-    const bool has_next = tn < ntiles;
+    // ---- plan and issue the next window
     Window Wn{0, 0};
-    uint32_t off_n = 0, end_n = 0;
-    bool valid_n = false;
-    if (has_next) {  // next tile's first window streams in while this tile decodes
-      valid_n = desc_read(tn, cur ^ 1u, off_n, end_n);
-      Wn = plan_window<STAGE>(valid_n && end_n - off_n <= fits, off_n, end_n);
-      issue_window<SWZ>(P.data, Wn, bufs + (cur ^ 1u) * STAGE, L);
+    uint32_t cov_n = 0;
+    bool has_next = false, new_tile = false;
+    if (__any(pend_p != 0)) {  // more of the planner's tile
+      Wn = plan_window<STAGE>(pend_p != 0, off_p, end_p);
+      has_next = true;
+    } else if (tp + nwaves < ntiles) {  // the next tile's first window
+      tp += nwaves;
+      slot ^= 1u;
+      valid_p = desc_read(tp, slot, off_p, end_p);
+      pend_p = (valid_p && end_p - off_p <= fits) ? 1u : 0u;
+      Wn = plan_window<STAGE>(pend_p != 0, off_p, end_p);
+      has_next = new_tile = true;
     }
-    desc_issue(tn + nwaves, cur);  // slot `cur` (tile t's) was read one iteration ago
-
-    const uint32_t i = t * 64u + lane;
+    nwait = 0;
+    if (has_next) {
+      cov_n = covered(Wn, pend_p, off_p, end_p);
+      pend_p &= cov_n ^ 1u;
+      issue_window<SWZ>(P.data, Wn, bufs + (cur ^ 1u) * STAGE, L, nt);
+      if (new_tile) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read before it is restaged
+        nwait = desc_issue(tp + 2u * nwaves, slot);
+      }
+    }
+    // ---- decode window cur (tile td, the lanes it covers)
+    const uint32_t i = td * 64u + lane;
+    const uint32_t clen = end_d - off_d;
+    if (first_d && big_d) {  // larger than a window
+      if constexpr (FAST) fb = 1;
+      else res = decode_packet<EXT>(GlbSrc{P.data, off_d}, clen, T, P.first, options,
+                                    EXT ? P.ext + i : nullptr);
+    }
     const uint32_t buf = bufs + cur * STAGE;
-    const uint32_t clen = end - off;
-    bool pending = valid, fallback = false;
-    if (pending && clen > fits) {  // larger than a window
+    if (cov_d && (P.options & kDiagSkipDecode)) {  // diagnostics: data movement only
+      res = Out{g_lds[buf + ((off_d - Wd.base) & ~15u)], 0, 0, 0, 0};
+    } else if (cov_d) {
+      const LdsSrc<SWZ> src{buf, off_d - Wd.base};
       if constexpr (FAST) {
-        fallback = true;
-      } else {  // straight from global memory
-        store_out(P, i, decode_packet<EXT>(GlbSrc{P.data, off}, clen, T, P.first, options,
-                                           EXT ? P.ext + i : nullptr));
+        const FastCtx F{P.eth_mult, ((uint32_t)GPD_LT_PAYLOAD << 8) | T.lut(GPD_LT_PAYLOAD),
+                        (options & GPD_OPT_IGNORE_UNSUPPORTED) ? GPD_ST_OK : GPD_ST_UNSUPPORTED};
+        if (!fast_decode<CS, HASH>(src.phys(src.pos), clen, F, res)) fb = 1;
+      } else {
+        res = decode_packet<EXT>(src, clen, T, P.first, options, EXT ? P.ext + i : nullptr);
       }
-      pending = false;
     }
-    bool firstw = true;
-    while (__any(pending)) {
-      if (!firstw) {  // further windows of this tile (tiles wider than a window)
-        W = plan_window<STAGE>(pending, off, end);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        issue_window<SWZ>(P.data, W, buf, L);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      firstw = false;
-      const bool in = pending && off >= W.base && end - W.base <= (uint32_t)STAGE;
-      if (in && (P.options & kDiagSkipDecode)) {  // diagnostics: data movement only
-        store_out(P, i, Out{g_lds[buf + ((off - W.base) & ~15u)], 0, 0, 0, 0});
-        pending = false;
-      } else if (in) {
-        const LdsSrc<SWZ> src{buf, off - W.base};
-        if constexpr (FAST) {
-          const FastCtx F{P.eth_mult, ((uint32_t)GPD_LT_PAYLOAD << 8) | T.lut(GPD_LT_PAYLOAD),
-                          (options & GPD_OPT_IGNORE_UNSUPPORTED) ? GPD_ST_OK : GPD_ST_UNSUPPORTED};
-          Out o;
-          if (fast_decode<CS, HASH>(src.phys(src.pos), clen, F, o))
-            store_out(P, i, o);
-          else
-            fallback = true;
-        } else {
-          store_out(P, i, decode_packet<EXT>(src, clen, T, P.first, options,
-                                             EXT ? P.ext + i : nullptr));
+    // ---- the tile is complete when the next window belongs to another tile (or none)
+    if (!has_next || new_tile) {
+      if (valid_d) store_out(P, i, res);  // a fallback lane's entry is rewritten by list_kernel
+      nwait += nst;
+      if constexpr (FAST) {  // append the tile's leftovers to the fallback list
+        const uint64_t m = __ballot(fb != 0);
+        if (m) {
+          uint32_t base = 0;
+          if (lane == (uint32_t)__builtin_ctzll(m)) base = atomicAdd(P.fb_count, (uint32_t)__popcll(m));
+          base = __builtin_amdgcn_readlane(base, (int)__builtin_ctzll(m));
+          if (fb) P.fb_list[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                        __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = i;
         }
-        pending = false;
       }
-    }
-    if constexpr (FAST) {  // append this tile's leftovers to the fallback list
-      const uint64_t m = __ballot(fallback);
-      if (m) {
-        uint32_t base = 0;
-        if (lane == (uint32_t)__builtin_ctzll(m)) base = atomicAdd(P.fb_count, (uint32_t)__popcll(m));
-        base = __builtin_amdgcn_readlane(base, (int)__builtin_ctzll(m));
-        if (fallback) P.fb_list[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = i;
-      }
+      fb = 0;
     }
     if (!has_next) break;
-    t = tn;
-    valid = valid_n;
-    off = off_n;
-    end = end_n;
-    W = Wn;
+    if (new_tile) {
+      td = tp;
+      off_d = off_p;
+      end_d = end_p;
+      valid_d = valid_p;
+      big_d = (valid_p && end_p - off_p > fits) ? 1u : 0u;
+      first_d = true;
+    } else {
+      first_d = false;
+    }
+    Wd = Wn;
+    cov_d = cov_n;
     cur ^= 1u;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of the freed buffer / slot done
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of the freed buffer done
   }
 }
 
@@ -1160,7 +1230,7 @@ __global__ __launch_bounds__(256) void list_kernel(KParams P) {
                      P.tcp_bits, P.udp_bits, P.eth_mult, P.tcp_mult, P.udp_mult};
   const uint32_t cnt = *P.fb_count;
   const uint32_t dlen = (uint32_t)P.data_len;
-  const uint32_t options = P.options & ~(kDiagSkipDecode | kDiagNoWait);
+  const uint32_t options = P.options & ~kDiagMask;
   for (uint32_t j = blockIdx.x * 256u + threadIdx.x; j < cnt; j += gridDim.x * 256u) {
     const uint32_t i = P.fb_list[j];
     const uint32_t off = min(P.offset[i], dlen);
@@ -1170,17 +1240,18 @@ __global__ __launch_bounds__(256) void list_kernel(KParams P) {
 }
 
 template <int STAGE, bool FAST, bool EXT, bool PAGES, bool SWZ, int WAVES, bool CS = true,
-          bool HASH = true>
+          bool HASH = true, int MINW = 1>
 static hipError_t launch_t(const KParams &P, hipStream_t stream, int num_cus) {
   const uint64_t ntiles = (P.n + 63) / 64;
   const size_t img = (P.image_words * 4u + 15u) & ~15u;
   const size_t lds = img + (size_t)(STAGE * 2 + 1024) * WAVES + 64;  // + slack past the last slot
   const uint64_t per_cu = (160u * 1024u) / lds;                       // resident workgroups per CU
   uint64_t blocks = (ntiles + WAVES - 1) / WAVES;
-  const uint64_t cap = (uint64_t)num_cus * (per_cu ? per_cu : 1) * 4;  // a few tiles per wave
+  static const int rounds = getenv("GPD_ROUNDS") ? atoi(getenv("GPD_ROUNDS")) : 4;  // A/B only
+  const uint64_t cap = (uint64_t)num_cus * (per_cu ? per_cu : 1) * (rounds > 0 ? rounds : 4);
   if (blocks > cap) blocks = cap;
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL((decode_kernel<STAGE, FAST, EXT, PAGES, SWZ, WAVES, CS, HASH>), dim3((unsigned)blocks),
+  hipLaunchKernelGGL((decode_kernel<STAGE, FAST, EXT, PAGES, SWZ, WAVES, CS, HASH, MINW>), dim3((unsigned)blocks),
                      dim3(64 * WAVES), lds, stream, P);
   return hipGetLastError();
 }
@@ -1198,6 +1269,11 @@ static int geom() {
 // the fast kernel reads headers at any byte address: linear windows
 template <bool CS, bool HASH>
 static hipError_t launch_fast(const KParams &P, hipStream_t stream, int num_cus) {
+  if (geom() == 2) {  // A/B: register budget for 4 waves per SIMD
+    if (P.stage == 4096)
+      return launch_t<4096, true, false, false, false, 4, CS, HASH, 4>(P, stream, num_cus);
+    return launch_t<8192, true, false, false, false, 4, CS, HASH, 4>(P, stream, num_cus);
+  }
   if (P.stage == 4096)
     return launch_t<4096, true, false, false, false, 4, CS, HASH>(P, stream, num_cus);
   return launch_t<8192, true, false, false, false, 4, CS, HASH>(P, stream, num_cus);

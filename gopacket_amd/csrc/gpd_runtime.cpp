@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <vector>
@@ -410,9 +411,18 @@ static int launch(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, hipS
   // LDS window per buffer: the smallest of 4/8 KiB that holds a typical 64-packet tile
   const uint64_t mean_slot = (in->data_len + in->n - 1) / in->n;
   P.stage = mean_slot * 64 <= 4096 ? 4096u : 8192u;
+  {  // A/B only: force the window size
+    static const char *st = getenv("GPD_STAGE");
+    if (st) P.stage = atoi(st) == 8192 ? 8192u : 4096u;
+  }
   P.first = ctx->first;
   P.decoders = ctx->decoders;
   P.options = ctx->options;
+  {  // streamed bytes and results use the nt cache policy (read once / written once);
+     // GPD_DIAG=<0..3> overrides the two bits for A/B runs only
+    static const char *d = getenv("GPD_DIAG");
+    P.options |= (d ? ((uint32_t)atoi(d) & 3u) : 3u) << 28;
+  }
   P.nstores = 2u + (out->net_hash != nullptr) + (out->tp_hash != nullptr) + (out->csum != nullptr);
   if (gpd::fast_eligible(P)) {  // fallback list scratch for this stream, sized for one launch
     const uint64_t need = std::min<uint64_t>(in->n, gpd::kMaxLaunchPackets);
