@@ -714,6 +714,49 @@ __device__ __forceinline__ void load80(uint32_t (&W)[20], uint32_t a) {
   }
 }
 
+// A long transport segment left to the wave-cooperative sum (COOP): its partial LE-domain
+// sum (pseudo-header, head and tail chunks) and the aligned 16-byte chunks [a, b) of the
+// window between them, whose sum is a difference of the window's chunk prefix sums.
+struct Seg {
+  uint32_t part, a, b;
+};
+
+// Inclusive prefix sum over the 64 lanes: row shifts 1/2/4/8, then row broadcasts 15 / 31.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
+  return v;
+}
+
+// P[c] = LE-domain sum of the window's 16-byte chunks below c, for c in [0, 512], written
+// to LDS at pfx.  Lane l sums chunks [8l, 8l + 8); bytes past the window's end only reach
+// entries beyond it.
+__device__ __forceinline__ void window_prefix(uint32_t buf, uint32_t pfx, uint32_t lane) {
+  uint32_t c[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const uint4 q = *reinterpret_cast<const uint4 *>(g_lds + buf + 128u * lane + 16u * j);
+    c[j] = dot2(q.w, 0x00010001u, dot2(q.z, 0x00010001u,
+                dot2(q.y, 0x00010001u, dot2(q.x, 0x00010001u, 0u))));
+  }
+  uint32_t run = 0;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const uint32_t v = c[j];
+    c[j] = run;  // exclusive within the block
+    run += v;
+  }
+  const uint32_t incl = wave_incl_scan(run), base = incl - run;
+  uint4 *d = reinterpret_cast<uint4 *>(g_lds + pfx + 32u * lane);
+  d[0] = uint4{base + c[0], base + c[1], base + c[2], base + c[3]};
+  d[1] = uint4{base + c[4], base + c[5], base + c[6], base + c[7]};
+  if (lane == 63u) *reinterpret_cast<uint32_t *>(g_lds + pfx + 2048u) = incl;
+}
+
 // p: LDS address of the packet's first byte; len: its length.  CS / HASH: the fused
 // checksums / flow hashes are requested (GPD_OPT_NO_CHECKSUMS / _NO_FLOW_HASH clear).
 // Two dependent LDS round trips per pass (three for tagged frames): (1) the Ethernet header
@@ -723,8 +766,10 @@ __device__ __forceinline__ void load80(uint32_t (&W)[20], uint32_t a) {
 // lookups then confirm the guesses; a packet they contradict goes to the generic decoder.
 // Hashes and checksums are computed from registers as each layer is accepted, so VXLAN's
 // second pass overwrites them exactly as the reused layer objects are overwritten (A11).
-template <bool CS, bool HASH>
-__device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const FastCtx &F, Out &o) {
+// COOP: a long even-aligned segment's whole middle chunks are left to window_prefix (sg).
+template <bool CS, bool HASH, bool COOP>
+__device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const FastCtx &F, Out &o,
+                                            uint32_t buf, Seg &sg) {
   uint64_t codes = 0, nh = 0, th = 0;
   uint32_t nc = 0, trunc = 0, stop = 0;
   uint32_t net = 0, tp = 0, ip4 = 0, ipcs = 0;
@@ -873,6 +918,41 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
   if (HASH) {
     st |= (1u << 16) | (net << 20) | (tp ? (1u << 17) | ((tp == 1 ? 4u : 5u) << 24) : 0u);
   }
+  sg.b = 0;
+  if (COOP && CS && tp && tp_len >= 64u && !((p + tp_off) & 1u)) {
+    // head [S, A) and tail [B, E) from their aligned chunks; [A, B) from the prefix sums
+    const uint32_t S = p + tp_off, E = S + tp_len, A = (S + 15u) & ~15u, B = E & ~15u;
+    uint32_t s = tp_ps;
+    if (A > S) {  // keep bytes from S & 15 on
+      const uint4 q = *reinterpret_cast<const uint4 *>(g_lds + A - 16u);
+      const uint32_t h8 = (S & 15u) * 8u;
+      uint64_t lo = ((uint64_t)q.y << 32) | q.x, hi = ((uint64_t)q.w << 32) | q.z;
+      lo = h8 >= 64u ? 0ull : (lo >> h8) << h8;
+      hi = h8 > 64u ? (hi >> (h8 - 64u)) << (h8 - 64u) : hi;
+      s = dot2((uint32_t)lo, 0x00010001u, s);
+      s = dot2((uint32_t)(lo >> 32), 0x00010001u, s);
+      s = dot2((uint32_t)hi, 0x00010001u, s);
+      s = dot2((uint32_t)(hi >> 32), 0x00010001u, s);
+    }
+    if (E > B) {  // keep bytes below E & 15
+      const uint4 q = *reinterpret_cast<const uint4 *>(g_lds + B);
+      const uint32_t r8 = (E & 15u) * 8u;
+      uint64_t lo = ((uint64_t)q.y << 32) | q.x, hi = ((uint64_t)q.w << 32) | q.z;
+      lo = r8 >= 64u ? lo : (lo << (64u - r8)) >> (64u - r8);
+      hi = r8 > 64u ? (hi << (128u - r8)) >> (128u - r8) : 0ull;
+      s = dot2((uint32_t)lo, 0x00010001u, s);
+      s = dot2((uint32_t)(lo >> 32), 0x00010001u, s);
+      s = dot2((uint32_t)hi, 0x00010001u, s);
+      s = dot2((uint32_t)(hi >> 32), 0x00010001u, s);
+    }
+    sg = Seg{s, (A - buf) >> 4, (B - buf) >> 4};
+    o.status = st | (ip4 ? 1u << 18 : 0u) | (1u << 19);
+    o.layers = codes | (stop & 0xFFFFu);
+    o.net_hash = HASH ? nh : 0;
+    o.tp_hash = HASH ? th : 0;
+    o.csum = ip4 ? ipcs : 0u;  // the transport half is added by the caller
+    return true;
+  }
   if (CS) {
     // TCP.ComputeChecksum(), tcp.go:193-195 / tcpip.go:52-88 over the last transport
     uint32_t s = tp_ps;
@@ -938,10 +1018,10 @@ struct Window {
   uint32_t base, nbytes;
 };
 
-// The first window of a tile starts at the first pending packet (rounded down to 16) and
-// covers every pending packet lying wholly inside [base, base + STAGE).  Packets normally
-// sit in lane order, so lane 63's end is the extent; a full wave maximum only runs when some
-// lane proves otherwise.
+// A window starts at the first pending packet (rounded down to 16) and covers every pending
+// packet lying wholly inside [base, base + STAGE).  Packets normally sit in lane order, so
+// the last covered lane's end is the extent; a full wave maximum only runs when some lane
+// proves otherwise.
 template <int STAGE>
 __device__ __forceinline__ Window plan_window(bool pending, uint32_t off, uint32_t end) {
   Window w{0, 0};
@@ -950,7 +1030,8 @@ __device__ __forceinline__ Window plan_window(bool pending, uint32_t off, uint32
   w.base = __builtin_amdgcn_readlane(off, (int)__builtin_ctzll(m)) & ~15u;
   const bool in = pending && off >= w.base && end - w.base <= (uint32_t)STAGE;
   const uint32_t x = in ? end - w.base : 0u;
-  uint32_t need = __builtin_amdgcn_readlane(x, 63);
+  const uint64_t mi = __ballot(in);  // nonzero: the first pending lane is in
+  uint32_t need = __builtin_amdgcn_readlane(x, 63 - (int)__builtin_clzll(mi));  // last lane in
   if (__any(x > need)) need = __builtin_amdgcn_readfirstlane(wave_max(x));
   w.nbytes = (need + 15u) & ~15u;
   return w;
@@ -1041,6 +1122,12 @@ __device__ __forceinline__ void wait_window(uint32_t nstores) {
   }
 }
 
+// LDS bytes per wave: two windows, two descriptor slots, and (fast kernel, 8 KiB windows)
+// the 513 chunk prefix sums of the cooperative segment checksum.
+__host__ __device__ constexpr uint32_t wave_lds_bytes(int stage, bool fast) {
+  return 2u * stage + 1024u + ((fast && stage == 8192) ? 2064u : 0u);
+}
+
 // WAVES waves per workgroup; each wave owns 64-packet tiles t, t + W, ... (grid stride).  A
 // tile's bytes are staged through LDS windows of STAGE bytes (a tile of large packets takes
 // several), and the window is the pipeline unit: per wave, LDS holds two window buffers
@@ -1066,9 +1153,11 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void decode_kernel(KParams P) {
   __syncthreads();
   const Tab<PAGES> T{P.pages,    P.eth_base, P.tcp_base, P.udp_base, P.eth_bits,
                      P.tcp_bits, P.udp_bits, P.eth_mult, P.tcp_mult, P.udp_mult};
+  constexpr bool COOP = FAST && STAGE == 8192;  // long segments: wave-cooperative checksum
   const uint32_t img = (P.image_words * 4u + 15u) & ~15u;
-  const uint32_t bufs = img + wave * (2u * STAGE + 1024u);
+  const uint32_t bufs = img + wave * wave_lds_bytes(STAGE, FAST);
   const uint32_t dslots = bufs + 2u * STAGE;  // two slots of 64 offsets + 64 caplens
+  const uint32_t pfx = dslots + 1024u;        // COOP: 513 chunk prefix sums
   const uint32_t n = (uint32_t)P.n;  // <= kMaxLaunchPackets per launch
   const uint32_t ntiles = (n + 63u) >> 6;
   const uint32_t nwaves = gridDim.x * WAVES;
@@ -1173,6 +1262,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void decode_kernel(KParams P) {
                                     EXT ? P.ext + i : nullptr);
     }
     const uint32_t buf = bufs + cur * STAGE;
+    Seg sg{0, 0, 0};
     if (cov_d && (P.options & kDiagSkipDecode)) {  // diagnostics: data movement only
       res = Out{g_lds[buf + ((off_d - Wd.base) & ~15u)], 0, 0, 0, 0};
     } else if (cov_d) {
@@ -1180,9 +1270,20 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void decode_kernel(KParams P) {
       if constexpr (FAST) {
         const FastCtx F{P.eth_mult, ((uint32_t)GPD_LT_PAYLOAD << 8) | T.lut(GPD_LT_PAYLOAD),
                         (options & GPD_OPT_IGNORE_UNSUPPORTED) ? GPD_ST_OK : GPD_ST_UNSUPPORTED};
-        if (!fast_decode<CS, HASH>(src.phys(src.pos), clen, F, res)) fb = 1;
+        if (!fast_decode<CS, HASH, COOP>(src.phys(src.pos), clen, F, res, buf, sg)) fb = 1;
       } else {
         res = decode_packet<EXT>(src, clen, T, P.first, options, EXT ? P.ext + i : nullptr);
+      }
+    }
+    if constexpr (COOP) {  // long segments of this window: chunk prefix sums, shared
+      if (__any(sg.b > sg.a)) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        window_prefix(buf, pfx, lane);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (sg.b > sg.a) {
+          const uint32_t mid = lds_u32(pfx + 4u * sg.b) - lds_u32(pfx + 4u * sg.a);
+          res.csum |= fold_le_not(sg.part + mid) << 16;
+        }
       }
     }
     // ---- the tile is complete when the next window belongs to another tile (or none)
@@ -1244,7 +1345,7 @@ template <int STAGE, bool FAST, bool EXT, bool PAGES, bool SWZ, int WAVES, bool 
 static hipError_t launch_t(const KParams &P, hipStream_t stream, int num_cus) {
   const uint64_t ntiles = (P.n + 63) / 64;
   const size_t img = (P.image_words * 4u + 15u) & ~15u;
-  const size_t lds = img + (size_t)(STAGE * 2 + 1024) * WAVES + 64;  // + slack past the last slot
+  const size_t lds = img + (size_t)wave_lds_bytes(STAGE, FAST) * WAVES + 64;  // + slack
   const uint64_t per_cu = (160u * 1024u) / lds;                       // resident workgroups per CU
   uint64_t blocks = (ntiles + WAVES - 1) / WAVES;
   static const int rounds = getenv("GPD_ROUNDS") ? atoi(getenv("GPD_ROUNDS")) : 4;  // A/B only
@@ -1329,7 +1430,8 @@ __global__ void probe_fast(KParams P) {
   Out o{};
   const FastCtx F{P.eth_mult, 0x2C8, 1};
   (void)T;
-  if (fast_decode<true, true>(pos, len, F, o)) store_out(P, threadIdx.x, o);
+  Seg sg{0, 0, 0};
+  if (fast_decode<true, true, false>(pos, len, F, o, 0, sg)) store_out(P, threadIdx.x, o);
 }
 }  // namespace gpd
 #endif
