@@ -74,6 +74,24 @@ def cpu_baseline(batch, budget_s: float = 10.0, max_threads: int = 16):
                       f"{threads} threads)"}
 
 
+def load_traffic(config: str):
+    """HBM bytes per launch of the decode kernel from the newest committed rocprofv3 summary
+    (profiles/rNN/<config>/summary.json, written by tools/prof_summary.py from separate
+    FETCH_SIZE / WRITE_SIZE passes with the gfx950 x2 FETCH_SIZE correction)."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", config, "summary.json")))
+    if not paths:
+        return None
+    try:
+        s = json.load(open(paths[-1]))
+    except (OSError, ValueError):
+        return None
+    k = [v for n, v in s.get("kernels", {}).items() if "decode_kernel" in n]
+    return {"read": s.get("hbm_read_bytes_per_launch"), "write": s.get("hbm_write_bytes_per_launch"),
+            "kernel_us": k[0]["avg_us"] if k else None,
+            "source": os.path.relpath(paths[-1], ROOT)}
+
+
 def dist_max(values, dist, device):
     """Max over ranks of a few floats (identity without torch.distributed)."""
     if not dist:
@@ -126,6 +144,9 @@ def main():
     ap.add_argument("--packets", type=int, default=0, help="override packets per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--host", action="store_true",
+                    help="diagnostic: PCIe-inclusive rate through gpd_decode_host (host arrays in, "
+                    "host arrays out); never the reported metric")
     ap.add_argument("--ablate", default="", help="diagnostics only: 'nocsum', 'nohash' or both "
                     "(comma separated); never used for the reported metric")
     args = ap.parse_args()
@@ -179,6 +200,28 @@ def main():
                           "GBps_read_plus_write": 2 * src.numel() / ms / 1e6}), flush=True)
         return
 
+    if args.host:  # PCIe-inclusive: repack into pinned slots, H2D, decode, D2H
+        res = parser.DecodeBatchHost(batch)
+        for _ in range(max(1, args.warmup // 2)):
+            parser.DecodeBatchHost(batch, out=res)
+        steps = max(1, min(args.steps, 5))
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            parser.DecodeBatchHost(batch, out=res)
+        el = time.perf_counter() - t0
+        n_err = int(np.count_nonzero((res.status & 3) != 0))
+        if rank == 0:
+            print(json.dumps({"metric": "DIAGNOSTIC (not the metric): PCIe-inclusive Mpackets/s "
+                              "host batch -> gpd_decode_host -> host results",
+                              "value": round(n * steps / el / 1e6, 2), "unit": "Mpackets/s",
+                              "ms_per_step": round(el / steps * 1e3, 3), "steps": steps,
+                              "config": {"workload": workload, "packets": n,
+                                         "host_bytes_in": int(batch.data_len) + 8 * n,
+                                         "decode_errors_in_batch": n_err},
+                              "GBps_in": round((batch.data_len + 8 * n) * steps / el / 1e9, 2)}),
+                  flush=True)
+        return
+
     for _ in range(args.warmup):
         parser.decode_device(dev_batch, dev_res, stream)
     torch.cuda.synchronize(local)
@@ -205,6 +248,12 @@ def main():
     n_err = int(np.count_nonzero((st & 3) != 0))
     out = summarize(workload, n, world, args.steps, args.warmup, elapsed, kern_ms, kern_ms_max,
                     batch, n_err)
+    tr = load_traffic(args.config) if n == n_default else None
+    if tr and tr["read"]:
+        out["roofline"]["traffic"] = int(tr["read"])
+        out["roofline"]["traffic_write"] = int(tr["write"]) if tr["write"] else None
+        out["roofline"]["traffic_source"] = tr["source"]
+        out["roofline"]["profiled_kernel_us"] = tr["kernel_us"]
     if args.ablate:
         out["ablation"] = args.ablate
         out["metric"] = "DIAGNOSTIC ablation (not the metric): " + out["metric"]

@@ -1324,12 +1324,14 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void decode_kernel(KParams P) {
 // global memory (these packets are rare outside crafted inputs).
 template <bool PAGES>
 __global__ __launch_bounds__(256) void list_kernel(KParams P) {
+  const uint32_t cnt = *P.fb_count;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *P.fb_next = 0;  // for the next fast launch
+  if (cnt <= blockIdx.x * 256u) return;  // nothing for this workgroup (usually: nothing at all)
   for (uint32_t k = threadIdx.x; k < P.image_words; k += 256)
     reinterpret_cast<uint32_t *>(g_lds)[k] = P.image[k];
   __syncthreads();
   const Tab<PAGES> T{P.pages,    P.eth_base, P.tcp_base, P.udp_base, P.eth_bits,
                      P.tcp_bits, P.udp_bits, P.eth_mult, P.tcp_mult, P.udp_mult};
-  const uint32_t cnt = *P.fb_count;
   const uint32_t dlen = (uint32_t)P.data_len;
   const uint32_t options = P.options & ~kDiagMask;
   for (uint32_t j = blockIdx.x * 256u + threadIdx.x; j < cnt; j += gridDim.x * 256u) {
@@ -1399,9 +1401,8 @@ bool fast_eligible(const KParams &P) {
 hipError_t launch_decode(const KParams &P, hipStream_t stream, int num_cus) {
   if (P.n > kMaxLaunchPackets) return hipErrorInvalidValue;
   if (fast_eligible(P)) {
-    if (!P.fb_count || !P.fb_list) return hipErrorInvalidValue;
-    hipError_t e = hipMemsetAsync(P.fb_count, 0, sizeof(uint32_t), stream);
-    if (e != hipSuccess) return e;
+    if (!P.fb_count || !P.fb_next || !P.fb_list) return hipErrorInvalidValue;
+    hipError_t e;
     const bool cs = !(P.options & GPD_OPT_NO_CHECKSUMS), hash = !(P.options & GPD_OPT_NO_FLOW_HASH);
     e = cs ? (hash ? launch_fast<true, true>(P, stream, num_cus)
                    : launch_fast<true, false>(P, stream, num_cus))

@@ -195,6 +195,7 @@ struct gpd_ctx {
   struct Fallback {
     uint32_t *d = nullptr;
     uint64_t cap = 0;
+    uint32_t parity = 0;
   };
   std::map<hipStream_t, Fallback> fallback;
   bool timing = false;
@@ -434,11 +435,12 @@ static int launch(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, hipS
         fb.d = nullptr;
         fb.cap = 0;
       }
-      HIP_TRY(hipMalloc(&fb.d, (need + 64) * sizeof(uint32_t)));
+      HIP_TRY(hipMalloc(&fb.d, (need + 128) * sizeof(uint32_t)));
+      HIP_TRY(hipMemset(fb.d, 0, 128 * sizeof(uint32_t)));  // both counters start at zero
       fb.cap = need;
+      fb.parity = 0;
     }
-    P.fb_count = fb.d;
-    P.fb_list = fb.d + 64;  // count in its own 256-byte line
+    P.fb_list = fb.d + 128;
   }
   if (record) HIP_TRY(hipEventRecord(ctx->ev0, stream));
   // launches of <= kMaxLaunchPackets packets keep every packet/tile index 32-bit in the kernel
@@ -453,6 +455,12 @@ static int launch(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, hipS
     Q.tp_hash = out->tp_hash ? out->tp_hash + lo : nullptr;
     Q.csum = out->csum ? out->csum + lo : nullptr;
     Q.ext = out->ext ? out->ext + lo : nullptr;
+    if (gpd::fast_eligible(P)) {  // two counters in their own lines, used alternately: each
+      auto &fb = ctx->fallback[stream];  // list kernel zeroes the one the next launch takes
+      Q.fb_count = fb.d + 64 * fb.parity;
+      Q.fb_next = fb.d + 64 * (fb.parity ^ 1u);
+      fb.parity ^= 1u;
+    }
     hipError_t e = gpd::launch_decode(Q, stream, ctx->num_cus);
     if (e != hipSuccess) return set_err(GPD_ERR_HIP, "decode kernel launch: %s", hipGetErrorString(e));
   }

@@ -240,12 +240,14 @@ class DecodingLayerParser:
         torch.cuda.synchronize(self.device)
         return dr.to_host()
 
-    def DecodeBatchHost(self, batch: PacketBatch, ext: bool = False) -> BatchResult:
-        """Host-memory path through gpd_decode_host (pinned, chunked, double-buffered)."""
+    def DecodeBatchHost(self, batch: PacketBatch, ext: bool = False,
+                        out: Optional[BatchResult] = None) -> BatchResult:
+        """Host-memory path through gpd_decode_host (pinned, chunked, double-buffered).
+        `out` reuses a result of the same size (no allocation per call)."""
         n = batch.n
-        res = BatchResult(np.zeros(n, np.uint32), np.zeros(n, np.uint64), np.zeros(n, np.uint64),
-                          np.zeros(n, np.uint64), np.zeros(n, np.uint32),
-                          np.zeros(n, EXT_DTYPE) if ext else None)
+        res = out if out is not None else BatchResult(
+            np.zeros(n, np.uint32), np.zeros(n, np.uint64), np.zeros(n, np.uint64),
+            np.zeros(n, np.uint64), np.zeros(n, np.uint32), np.zeros(n, EXT_DTYPE) if ext else None)
         b = GpdBatch(batch.data.ctypes.data, batch.data_len, batch.offset.ctypes.data,
                      batch.caplen.ctypes.data, n)
         r = GpdResult(res.status.ctypes.data, res.layers.ctypes.data, res.net_hash.ctypes.data,

@@ -1,0 +1,23 @@
+#!/bin/bash
+# rocprofv3 evidence for one bench config: kernel trace + stats, then separate PMC passes
+# (FETCH_SIZE, WRITE_SIZE, SQ instruction/wait counters).  Output: gpurun_out/prof/<cfg>/
+# usage: tools/prof_round.sh CFG [STEPS]
+set -u
+cd "${GRAFT_REPO_ROOT:-.}"
+export TMPDIR=/tmp
+CFG=$1
+STEPS=${2:-20}
+D=gpurun_out/prof/$CFG
+mkdir -p "$D"
+B="python3 bench.py --config $CFG --steps $STEPS --warmup 3 --no-cpu-baseline"
+run() {  # name, rocprofv3 args...
+  local name=$1; shift
+  timeout -k 10 400 rocprofv3 "$@" --output-format csv -d "$D/$name" -o "$name" -- $B > "$D/$name.log" 2>&1
+  local rc=$?
+  echo "$CFG $name rc=$rc"
+  return $rc
+}
+run kt --kernel-trace --stats &&
+run fetch --pmc FETCH_SIZE &&
+run write --pmc WRITE_SIZE &&
+run sq --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY
