@@ -38,6 +38,9 @@ CONFIGS = {
              "5-tuple flow hashes, synthetic seed 0x5EED0003", 1 << 22),
     "vxlan": ("config4: 2^23 x 128 B Eth/IPv4/UDP/VXLAN/Eth/IPv4/TCP, inner flow keys, "
               "synthetic seed 0x5EED0004", 1 << 23),
+    "pcap64": ("config5 (per GPU): a pcap capture of 2^24 x 64 B Eth/IPv4/UDP records decoded in "
+               "place (the capture bytes are the batch buffer: 16-B record headers interleaved), "
+               "records indexed by the native pcap walker; synthetic seed 0x5EED0002", 1 << 24),
 }
 
 
@@ -48,6 +51,9 @@ def make_batch(config: str, n: int, rank: int):
         return synth.make_udp64(n, 0x5EED0002 + seed_off)
     if config == "imix":
         return synth.make_imix(n, 0x5EED0003 + seed_off)
+    if config == "pcap64":
+        from gopacket_amd import pcap as NP
+        return NP.synth_capture(synth.make_udp64(n, 0x5EED0002 + seed_off))
     return synth.make_vxlan(n, 0x5EED0004 + seed_off)
 
 
@@ -102,11 +108,13 @@ def dist_max(values, dist, device):
     return [float(v) for v in t.cpu()]
 
 
-def summarize(workload, n, world, steps, warmup, elapsed, kern_ms, kern_ms_max, batch, n_err):
-    """The contract JSON object: `value` = packets all ranks decoded / max-over-ranks time."""
+def summarize(workload, n, world, steps, warmup, elapsed, kern_ms, kern_ms_max, batch, n_err,
+              interleaved=0):
+    """The contract JSON object: `value` = packets all ranks decoded / max-over-ranks time.
+    `interleaved`: bytes per packet the windows stream besides the packet (pcap record headers)."""
     total_pkts = n * world * steps
     value = total_pkts / elapsed / 1e6
-    read_bytes = int(batch.caplen.astype(np.int64).sum()) + DESC_BYTES * n
+    read_bytes = int(batch.caplen.astype(np.int64).sum()) + (DESC_BYTES + interleaved) * n
     write_bytes = 4 + 8 + 8 + 8 + 4  # status, layers, net_hash, tp_hash, csum per packet
     achieved = read_bytes / (kern_ms * 1e-3) / 1e9
     return {
@@ -135,6 +143,29 @@ def summarize(workload, n, world, steps, warmup, elapsed, kern_ms, kern_ms_max, 
     }
 
 
+def replay_pcap(parser, cap, n, total, threads):
+    """PCIe-inclusive rate: the capture in (registered) host memory replayed through
+    gpd_decode_pcap — native index, raw capture bytes H2D, decode, results D2H — until `total`
+    packets were decoded.  Diagnostic beside the device-resident value, never `value`."""
+    from gopacket_amd._lib import check, lib
+    check(lib.gpd_host_register(parser.ctx().h, cap.ctypes.data, cap.nbytes), "gpd_host_register")
+    try:
+        parser.DecodePcap(cap, nthreads=threads)  # warm: staging slots, streams
+        done, t0, reps = 0, time.perf_counter(), 0
+        while done < total:
+            res, k, err = parser.DecodePcap(cap, nthreads=threads)
+            assert err is None and k == n
+            done += k
+            reps += 1
+        el = time.perf_counter() - t0
+    finally:
+        lib.gpd_host_unregister(parser.ctx().h, cap.ctypes.data)
+    return {"packets": done, "replays": reps, "s": round(el, 3),
+            "Mpackets_per_s": round(done / el / 1e6, 1),
+            "GBps_capture_in": round(reps * (cap.nbytes - 64) / el / 1e9, 2),
+            "path": "registered host capture -> native index -> raw bytes H2D -> decode -> D2H"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -147,6 +178,11 @@ def main():
     ap.add_argument("--host", action="store_true",
                     help="diagnostic: PCIe-inclusive rate through gpd_decode_host (host arrays in, "
                     "host arrays out); never the reported metric")
+    ap.add_argument("--threads", type=int, default=0, help="host threads for the pcap walker "
+                    "(0 = all cores)")
+    ap.add_argument("--replay", type=int, default=0, help="pcap64: also replay the capture from "
+                    "host memory through gpd_decode_pcap until this many packets were decoded "
+                    "(PCIe-inclusive rate; a diagnostic beside the device-resident value)")
     ap.add_argument("--ablate", default="", help="diagnostics only: 'nocsum', 'nohash' or both "
                     "(comma separated); never used for the reported metric")
     args = ap.parse_args()
@@ -169,6 +205,18 @@ def main():
     workload, n_default = CONFIGS[args.config]
     n = args.packets or n_default
     batch = make_batch(args.config, n, rank)
+    pcap_info = None
+    if args.config == "pcap64":  # index the capture: its bytes become the batch buffer
+        from gopacket_amd import pcap as NP
+        cap = batch
+        t0 = time.perf_counter()
+        pc = NP.index(cap, nthreads=args.threads)
+        t_index = time.perf_counter() - t0
+        assert pc.err is None and pc.batch.n == n, (pc.err, pc.batch.n)
+        batch = pc.batch
+        pcap_info = {"capture_bytes": int(batch.data_len), "index_s": round(t_index, 4),
+                     "index_Mrec_per_s": round(n / t_index / 1e6, 1),
+                     "index_threads": NP.last_walk_stats()[0]}
     dev_batch = P.DeviceBatch(batch, local)
     dev_res = P.DeviceResult(n, local, ext=False)
     parser = P.NewDecodingLayerParser(L.LayerTypeEthernet, P.Ethernet(), P.Dot1Q(), P.IPv4(),
@@ -247,7 +295,11 @@ def main():
     st = dev_res.status.cpu().numpy().view(np.uint32)
     n_err = int(np.count_nonzero((st & 3) != 0))
     out = summarize(workload, n, world, args.steps, args.warmup, elapsed, kern_ms, kern_ms_max,
-                    batch, n_err)
+                    batch, n_err, interleaved=16 if pcap_info else 0)
+    if pcap_info:
+        out["pcap"] = pcap_info
+        if args.replay:
+            out["pcap"]["pcie_inclusive"] = replay_pcap(parser, cap, n, args.replay, args.threads)
     tr = load_traffic(args.config) if n == n_default else None
     if tr and tr["read"]:
         out["roofline"]["traffic"] = int(tr["read"])

@@ -31,6 +31,12 @@ class GpdResult(C.Structure):
                 ("tp_hash", C.c_void_p), ("csum", C.c_void_p), ("ext", C.c_void_p)]
 
 
+class GpdPcapInfo(C.Structure):
+    _fields_ = [("magic", C.c_uint32), ("big_endian", C.c_uint32), ("nano", C.c_uint32),
+                ("version_major", C.c_uint32), ("version_minor", C.c_uint32),
+                ("snaplen", C.c_uint32), ("linktype", C.c_uint32), ("reserved", C.c_uint32)]
+
+
 EXPORTS = {
     # name: (restype, argtypes)
     "gpd_abi_version": (C.c_int, []),
@@ -44,7 +50,21 @@ EXPORTS = {
     "gpd_ctx_set_timing": (C.c_int, [C.c_void_p, C.c_int]),
     "gpd_last_kernel_ms": (C.c_float, [C.c_void_p]),
     "gpd_last_error_string": (C.c_char_p, []),
+    # include/gpd_pcap.h
+    "gpd_pcap_header": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(GpdPcapInfo)]),
+    "gpd_pcap_index": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(GpdPcapInfo), C.c_uint64,
+                                 C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                 C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                 C.POINTER(C.c_int), C.c_int]),
+    "gpd_decode_pcap": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64,
+                                  C.POINTER(GpdResult), C.POINTER(C.c_uint64),
+                                  C.POINTER(C.c_uint64), C.POINTER(C.c_int), C.c_int]),
+    "gpd_pcap_last_stats": (None, [C.POINTER(C.c_int)] * 3),
+    "gpd_host_register": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
+    "gpd_host_unregister": (C.c_int, [C.c_void_p, C.c_void_p]),
 }
+
+GPD_ERR_PCAP = -5
 
 
 class GpdError(RuntimeError):

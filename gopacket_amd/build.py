@@ -21,8 +21,10 @@ ARCH = os.environ.get("GPD_OFFLOAD_ARCH", "gfx950")
 LIB = os.path.join(PKG, "libgpd.so")
 ORACLE_LIB = os.path.join(ROOT, "oracle", "libgpd_oracle.so")
 
-SOURCES = [os.path.join(CSRC, "gpd_kernels.hip"), os.path.join(CSRC, "gpd_runtime.cpp")]
-HEADERS = [os.path.join(CSRC, "gpd_internal.h"), os.path.join(ROOT, "include", "gpd.h")]
+SOURCES = [os.path.join(CSRC, "gpd_kernels.hip"), os.path.join(CSRC, "gpd_runtime.cpp"),
+           os.path.join(CSRC, "gpd_pcap.cpp")]
+HEADERS = [os.path.join(CSRC, "gpd_internal.h"), os.path.join(ROOT, "include", "gpd.h"),
+           os.path.join(ROOT, "include", "gpd_pcap.h")]
 
 
 def _stale(target, deps):
@@ -35,7 +37,7 @@ def _stale(target, deps):
 def build_lib(force: bool = False, verbose: bool = False) -> str:
     if force or _stale(LIB, SOURCES + HEADERS):
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-               "-Wall", "-Wno-unused-function", "-I", os.path.join(ROOT, "include"),
+               "-Wall", "-Wno-unused-function", "-pthread", "-I", os.path.join(ROOT, "include"),
                *SOURCES, "-o", LIB + ".tmp"]
         if verbose:
             print(" ".join(cmd), flush=True)

@@ -85,6 +85,48 @@ constexpr uint64_t kMaxLaunchPackets = 1ull << 30;
 // Launch the decode kernel over P (asynchronous on `stream`).
 hipError_t launch_decode(const KParams &P, hipStream_t stream, int num_cus);
 
+// Host side: set the thread's gpd_last_error_string() text and return `code` (gpd_runtime.cpp).
+int set_error(int code, const char *fmt, ...);
+
+// Host side: the sequential pcap record walk over buf[pos:len), built in parallel
+// (gpd_pcap.cpp; semantics in include/gpd_pcap.h).  Positions are record-header offsets.
+}  // namespace gpd
+#include "../../include/gpd_pcap.h"
+#include <vector>
+namespace gpd {
+struct Recs {  // one walked stretch of records
+  std::vector<uint64_t> pos;  // record header positions
+  std::vector<uint32_t> cap, wire;
+  std::vector<uint64_t> ts;
+  void reserve(size_t n) {
+    pos.reserve(n);
+    cap.reserve(n);
+    wire.reserve(n);
+    ts.reserve(n);
+  }
+  size_t size() const { return pos.size(); }
+  void push(uint64_t p, uint32_t c, uint32_t w, uint64_t t) {
+    pos.push_back(p);
+    cap.push_back(c);
+    wire.push_back(w);
+    ts.push_back(t);
+  }
+};
+struct PcapSlice {
+  size_t r, j0, cnt;  // records [j0, j0+cnt) of stretch r
+};
+struct PcapWalk {
+  std::vector<Recs> R;          // per segment, then sequential re-walks
+  std::vector<PcapSlice> plan;  // the walk, in order
+  uint64_t n = 0, next_pos = 0;
+  int stop = 0, threads = 0, met = 0, rewalks = 0;
+  uint32_t a0 = 0, a1 = 0;
+};
+int pcap_walk(const uint8_t *buf, uint64_t len, const gpd_pcap_info &I, uint64_t pos, uint64_t max_n,
+              int nthreads, PcapWalk &W);
+void pcap_emit(const PcapWalk &W, uint64_t base, uint32_t *off32, uint64_t *pos64, uint32_t *cap,
+               uint32_t *wire, uint64_t *ts);
+
 // Multiplicative hash of a 16-bit key into 2^bits buckets (host and device must agree).
 __host__ __device__ inline uint32_t key_hash(uint32_t key, uint32_t mult, uint32_t bits) {
   return ((key * mult) & 0xFFFFu) >> (16 - bits);

@@ -46,6 +46,28 @@ constexpr uint32_t kDiagMask = kDiagSkipDecode | kDiagNoWait | kDiagNtLoad | kDi
 
 extern __shared__ __attribute__((aligned(16))) uint8_t g_lds[];
 
+#ifdef GPD_PHASE_TIMING
+// Diagnostic build only (libgpd_phase.so): per-phase shader-clock totals of the fast kernel's
+// loop, summed over waves; read back with gpd_diag_phase().
+__device__ unsigned long long g_phase[8];
+#define PH_DECL uint64_t ph_t = __builtin_amdgcn_s_memtime(), ph_acc[6] = {0, 0, 0, 0, 0, 0};
+#define PH_MARK(k)                                      \
+  do {                                                  \
+    const uint64_t ph_n = __builtin_amdgcn_s_memtime(); \
+    ph_acc[k] += ph_n - ph_t;                           \
+    ph_t = ph_n;                                        \
+  } while (0)
+#define PH_FLUSH                                                              \
+  do {                                                                        \
+    if (lane == 0)                                                            \
+      for (int k = 0; k < 6; k++) atomicAdd(&g_phase[k], (unsigned long long)ph_acc[k]); \
+  } while (0)
+#else
+#define PH_DECL
+#define PH_MARK(k) do {} while (0)
+#define PH_FLUSH do {} while (0)
+#endif
+
 __device__ __forceinline__ uint32_t lds_u32(uint32_t a) {
   return *reinterpret_cast<const uint32_t *>(g_lds + a);
 }
@@ -1214,7 +1236,9 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void decode_kernel(KParams P) {
   uint32_t cur = 0;  // buffer of the window to decode
   Out res{0, 0, 0, 0, 0};
   uint32_t fb = 0;
+  PH_DECL
   for (;;) {
+    PH_MARK(5);  // loop overhead / tail of the previous iteration
     // window cur landed: wait for all but the VMEM instructions issued after it
     if (!(P.options & kDiagNoWait)) {
       switch (nwait) {
@@ -1228,6 +1252,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void decode_kernel(KParams P) {
         default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
       }
     }
+    PH_MARK(0);  // waiting for the window
     // ---- plan and issue the next window
     Window Wn{0, 0};
     uint32_t cov_n = 0;
@@ -1253,6 +1278,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void decode_kernel(KParams P) {
         nwait = desc_issue(tp + 2u * nwaves, slot);
       }
     }
+    PH_MARK(1);  // planning and issuing the next window
     // ---- decode window cur (tile td, the lanes it covers)
     const uint32_t i = td * 64u + lane;
     const uint32_t clen = end_d - off_d;
@@ -1275,6 +1301,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void decode_kernel(KParams P) {
         res = decode_packet<EXT>(src, clen, T, P.first, options, EXT ? P.ext + i : nullptr);
       }
     }
+    PH_MARK(2);  // decode
     if constexpr (COOP) {  // long segments of this window: chunk prefix sums, shared
       if (__any(sg.b > sg.a)) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1286,6 +1313,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void decode_kernel(KParams P) {
         }
       }
     }
+    PH_MARK(3);  // cooperative checksum
     // ---- the tile is complete when the next window belongs to another tile (or none)
     if (!has_next || new_tile) {
       if (valid_d) store_out(P, i, res);  // a fallback lane's entry is rewritten by list_kernel
@@ -1302,7 +1330,11 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void decode_kernel(KParams P) {
       }
       fb = 0;
     }
-    if (!has_next) break;
+    PH_MARK(4);  // result stores, fallback list
+    if (!has_next) {
+      if constexpr (FAST) PH_FLUSH;
+      break;
+    }
     if (new_tile) {
       td = tp;
       off_d = off_p;
@@ -1420,6 +1452,18 @@ hipError_t launch_decode(const KParams &P, hipStream_t stream, int num_cus) {
 }
 
 }  // namespace gpd
+
+#ifdef GPD_PHASE_TIMING
+extern "C" int gpd_diag_phase(unsigned long long *out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gpd::g_phase), 6 * sizeof(unsigned long long)) != hipSuccess)
+    return -1;
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(gpd::g_phase), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 #ifdef GPD_ISA_PROBE
 // Instruction-count probe (not built into libgpd.so): the fast path alone on one packet.

@@ -1,0 +1,337 @@
+// gpd_pcap.cpp — pcap record walk, host side of include/gpd_pcap.h.
+//
+// Restates pcapgo's reader on an in-memory capture (paths relative to google/gopacket):
+//   readHeader ........ pcapgo/read.go:78-117   (magics read.go:47-49, write.go:32; v2.4)
+//   ReadPacketData .... pcapgo/read.go:120-137  (snaplen / original-length checks)
+//   readPacketHeader .. pcapgo/read.go:165-177  (timestamp = time.Unix(sec, uint32(frac*factor)))
+// Instead of copying each record out, the walk returns where each record's bytes lie in the
+// capture, so the capture buffer itself is the decoder's batch buffer.
+//
+// The walk is a linked list (each record header gives the next record's position).  With
+// several threads the buffer is cut into segments; every segment but the first is walked
+// speculatively from the first position whose header chain looks like pcap records, and the
+// segments are stitched in order: the true walk (segment 0, exact) ends at its first record
+// header at or past the next segment's start, and if the speculative walk of that segment
+// visited the same position, both walks coincide from there on (the list is deterministic),
+// so the speculative records from that position on are the true ones.  A segment whose
+// speculation the true walk never meets is re-walked sequentially.  The result is therefore
+// the sequential walk's for every input; speculation only decides how much of it runs in
+// parallel.
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "gpd_internal.h"
+#include "../../include/gpd_pcap.h"
+
+namespace gpd {
+
+namespace {
+
+inline uint32_t rd32(const uint8_t *p, bool be) {
+  uint32_t v;
+  std::memcpy(&v, p, 4);
+  return be ? __builtin_bswap32(v) : v;
+}
+inline uint16_t rd16(const uint8_t *p, bool be) {
+  uint16_t v;
+  std::memcpy(&v, p, 2);
+  return be ? (uint16_t)__builtin_bswap16(v) : v;
+}
+
+struct End {
+  uint64_t pos = 0;  // next record header position (the exit of a segment walk, or the stop)
+  int stop = GPD_PCAP_STOP_LIMIT;
+  uint32_t a0 = 0, a1 = 0;  // error arguments
+  bool stopped = false;     // the walk ended for good (EOF or a rejected record)
+};
+
+// One ReadPacketData step at position p: 1 = a record (fields set), 0 = the walk stops (e set).
+inline int step(const uint8_t *buf, uint64_t len, const gpd_pcap_info &I, uint64_t p, uint32_t &cap,
+                uint32_t &wire, uint64_t &ts, End &e) {
+  const uint64_t avail = len - p;
+  const bool be = I.big_endian != 0;
+  if (avail == 0) {  // io.ReadFull of the header reads nothing: io.EOF, the normal end
+    e.stop = GPD_PCAP_STOP_EOF;
+    return 0;
+  }
+  if (avail < GPD_PCAP_RECORD_BYTES) {  // read.go:166-168, io.ErrUnexpectedEOF
+    e.stop = GPD_PCAP_STOP_SHORT_HDR;
+    return 0;
+  }
+  const uint8_t *h = buf + p;
+  cap = rd32(h + 8, be);
+  wire = rd32(h + 12, be);
+  if (cap > I.snaplen) {  // read.go:125-127
+    e.stop = GPD_PCAP_STOP_SNAPLEN;
+    e.a0 = cap;
+    e.a1 = I.snaplen;
+    return 0;
+  }
+  if (cap > wire) {  // read.go:129-131
+    e.stop = GPD_PCAP_STOP_ORIGLEN;
+    e.a0 = cap;
+    e.a1 = wire;
+    return 0;
+  }
+  if (avail - GPD_PCAP_RECORD_BYTES < cap) {  // read.go:133-134, io.ReadFull of the data
+    e.stop = GPD_PCAP_STOP_SHORT_DATA;
+    e.a0 = (uint32_t)(avail - GPD_PCAP_RECORD_BYTES);  // 0 => io.EOF, else ErrUnexpectedEOF
+    return 0;
+  }
+  const uint32_t factor = I.nano ? 1u : 1000u;
+  ts = (uint64_t)rd32(h, be) * 1000000000ull + (uint32_t)(rd32(h + 4, be) * factor);  // read.go:172
+  return 1;
+}
+
+// Walk from p while record headers start before `limit`, at most max_n records.
+void walk(const uint8_t *buf, uint64_t len, const gpd_pcap_info &I, uint64_t p, uint64_t limit,
+          uint64_t max_n, Recs &out, End &e) {
+  uint64_t n = 0;
+  while (p < limit) {
+    if (n == max_n) {
+      e.stop = GPD_PCAP_STOP_LIMIT;
+      e.pos = p;
+      e.stopped = true;
+      return;
+    }
+    uint32_t cap, wire;
+    uint64_t ts;
+    if (!step(buf, len, I, p, cap, wire, ts, e)) {
+      e.pos = p;
+      e.stopped = true;
+      return;
+    }
+    out.push(p, cap, wire, ts);
+    n++;
+    p += GPD_PCAP_RECORD_BYTES + (uint64_t)cap;
+    // the chain only moves forward through contiguous records: stream the bytes ahead of it
+    // so each dependent header read hits the cache instead of paying DRAM latency
+    __builtin_prefetch(buf + std::min(p + 2048, len), 0, 0);
+    __builtin_prefetch(buf + std::min(p + 4096, len), 0, 0);
+  }
+  e.pos = p;  // exit: the first record header at or past `limit`
+  e.stopped = false;
+}
+
+// A header at x that, with the `depth` headers after it, passes every check of a record.
+bool plausible_chain(const uint8_t *buf, uint64_t len, const gpd_pcap_info &I, uint64_t x, int depth) {
+  End e;
+  for (int k = 0; k < depth; k++) {
+    if (x == len) return k > 0;  // the chain reaches the end of the capture exactly
+    uint32_t cap, wire;
+    uint64_t ts;
+    if (!step(buf, len, I, x, cap, wire, ts, e)) return false;
+    x += GPD_PCAP_RECORD_BYTES + (uint64_t)cap;
+  }
+  return true;
+}
+
+thread_local int g_last_threads = 0, g_last_rewalks = 0, g_last_met = 0;
+
+// nthreads <= 0: the machine's cores, at most 16 (a GPU's share of a shared host)
+int default_threads() { return (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency())); }
+
+}  // namespace
+
+// The sequential walk's result over buf[pos:len) (see gpd_pcap.h), built in parallel: per
+// segment record lists plus the in-order plan of slices that make up the walk.
+int pcap_walk(const uint8_t *buf, uint64_t len, const gpd_pcap_info &I, uint64_t pos, uint64_t max_n,
+              int nthreads, PcapWalk &W) {
+  W = PcapWalk{};
+  if (nthreads <= 0) nthreads = default_threads();
+  const uint64_t span = len > pos ? len - pos : 0;
+  const uint64_t kMinSeg = 4ull << 20;
+  int T = (int)std::min<uint64_t>((uint64_t)nthreads, std::max<uint64_t>(1, span / kMinSeg));
+  if (max_n < span / GPD_PCAP_RECORD_BYTES) T = 1;  // a bounded walk (a chunk): sequential
+  std::vector<uint64_t> seg(T + 1);
+  for (int k = 0; k <= T; k++) seg[k] = pos + span * (uint64_t)k / (uint64_t)T;
+  W.R.resize((size_t)T);
+  std::vector<End> E(T);
+  for (int k = 0; k < T; k++) W.R[k].reserve((size_t)((seg[k + 1] - seg[k]) / 96 + 16));
+  auto run = [&](int k) {
+    if (k == 0) {
+      walk(buf, len, I, pos, seg[1], T == 1 ? max_n : UINT64_MAX, W.R[0], E[0]);
+      return;
+    }
+    // speculation: the first position of the segment that starts a plausible chain
+    const uint64_t hi = std::min<uint64_t>(seg[k + 1], seg[k] + GPD_PCAP_RECORD_BYTES + (uint64_t)I.snaplen + 1);
+    for (uint64_t x = seg[k]; x < hi; x++) {
+      if (plausible_chain(buf, len, I, x, 8)) {
+        walk(buf, len, I, x, seg[k + 1], UINT64_MAX, W.R[k], E[k]);
+        return;
+      }
+    }
+    E[k].stopped = false;
+    E[k].pos = UINT64_MAX;  // no speculation
+  };
+  if (T == 1) {
+    run(0);
+  } else {
+    std::vector<std::thread> th;
+    for (int k = 1; k < T; k++) th.emplace_back(run, k);
+    run(0);
+    for (auto &t : th) t.join();
+  }
+  // stitch in order (no copies: the plan lists slices of the segment lists)
+  W.threads = T;
+  W.plan.push_back(PcapSlice{0, 0, W.R[0].size()});
+  End cur = E[0];
+  for (int k = 1; k < T && !cur.stopped; k++) {
+    if (cur.pos >= seg[k + 1]) continue;  // no true record starts in segment k
+    const auto &P = W.R[k].pos;
+    auto it = std::lower_bound(P.begin(), P.end(), cur.pos);
+    if (it != P.end() && *it == cur.pos) {  // the true walk meets the speculation
+      const size_t j = (size_t)(it - P.begin());
+      W.plan.push_back(PcapSlice{(size_t)k, j, P.size() - j});
+      cur = E[k];
+      W.met++;
+    } else {  // it never does: walk this segment sequentially
+      W.R.emplace_back();
+      End e;
+      walk(buf, len, I, cur.pos, seg[k + 1], UINT64_MAX, W.R.back(), e);
+      W.plan.push_back(PcapSlice{W.R.size() - 1, 0, W.R.back().size()});
+      cur = e;
+      W.rewalks++;
+    }
+  }
+  if (!cur.stopped) {  // the last segment ends at len: the next header starts exactly there
+    cur.stop = GPD_PCAP_STOP_EOF;
+    cur.stopped = true;
+  }
+  uint64_t n = 0;
+  for (auto &sl : W.plan) {  // apply max_n
+    if (n + sl.cnt > max_n) {
+      sl.cnt = (size_t)(max_n - n);
+      const size_t at = (size_t)(&sl - W.plan.data());
+      cur.pos = W.R[sl.r].pos[sl.j0 + sl.cnt];
+      W.plan.resize(at + 1);
+      cur.stop = GPD_PCAP_STOP_LIMIT;
+      cur.a0 = cur.a1 = 0;
+      n = max_n;
+      break;
+    }
+    n += sl.cnt;
+  }
+  if (n == max_n && cur.stop != GPD_PCAP_STOP_LIMIT) {  // as the sequential loop: the limit first
+    cur.stop = GPD_PCAP_STOP_LIMIT;
+    cur.a0 = cur.a1 = 0;
+  }
+  W.n = n;
+  W.next_pos = cur.pos;
+  W.stop = cur.stop;
+  W.a0 = cur.a0;
+  W.a1 = cur.a1;
+  g_last_threads = W.threads;
+  g_last_met = W.met;
+  g_last_rewalks = W.rewalks;
+  switch (W.stop) {
+    case GPD_PCAP_STOP_SHORT_HDR:
+      return set_error(GPD_ERR_PCAP, "unexpected EOF");
+    case GPD_PCAP_STOP_SNAPLEN:
+      return set_error(GPD_ERR_PCAP, "capture length exceeds snap length: %u > %u", W.a0, W.a1);
+    case GPD_PCAP_STOP_ORIGLEN:
+      return set_error(GPD_ERR_PCAP, "capture length exceeds original packet length: %u > %u", W.a0, W.a1);
+    case GPD_PCAP_STOP_SHORT_DATA:
+      return set_error(GPD_ERR_PCAP, W.a0 == 0 ? "EOF" : "unexpected EOF");
+    default:
+      return GPD_OK;
+  }
+}
+
+// Copy the walk into flat arrays (any pointer may be NULL), one thread per slice.
+//   off32[i] = pos + 16 - base, pos64[i] = pos, cap / wire / ts as walked
+void pcap_emit(const PcapWalk &W, uint64_t base, uint32_t *off32, uint64_t *pos64, uint32_t *cap,
+               uint32_t *wire, uint64_t *ts) {
+  std::vector<uint64_t> at(W.plan.size() + 1, 0);
+  for (size_t s = 0; s < W.plan.size(); s++) at[s + 1] = at[s] + W.plan[s].cnt;
+  auto one = [&](size_t s) {
+    const PcapSlice &sl = W.plan[s];
+    const Recs &r = W.R[sl.r];
+    const uint64_t o = at[s];
+    const uint64_t d = GPD_PCAP_RECORD_BYTES - base;  // wraps, as unsigned arithmetic intends
+    if (off32)
+      for (size_t j = 0; j < sl.cnt; j++) off32[o + j] = (uint32_t)(r.pos[sl.j0 + j] + d);
+    if (pos64) std::memcpy(pos64 + o, r.pos.data() + sl.j0, sl.cnt * 8);
+    if (cap) std::memcpy(cap + o, r.cap.data() + sl.j0, sl.cnt * 4);
+    if (wire) std::memcpy(wire + o, r.wire.data() + sl.j0, sl.cnt * 4);
+    if (ts) std::memcpy(ts + o, r.ts.data() + sl.j0, sl.cnt * 8);
+  };
+  if (W.plan.size() <= 1) {
+    if (!W.plan.empty()) one(0);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (size_t s = 1; s < W.plan.size(); s++) th.emplace_back(one, s);
+  one(0);
+  for (auto &t : th) t.join();
+}
+
+}  // namespace gpd
+
+extern "C" {
+
+int gpd_pcap_header(const uint8_t *buf, uint64_t len, gpd_pcap_info *info) {
+  if (!info || (!buf && len)) return gpd::set_error(GPD_ERR_INVALID, "gpd_pcap_header: null argument");
+  std::memset(info, 0, sizeof *info);
+  // bufio Peek(2) then io.ReadFull(24) (read.go:79-92)
+  if (len < 2) return gpd::set_error(GPD_ERR_PCAP, "EOF");
+  if (buf[0] == 0x1f && buf[1] == 0x8b)
+    return gpd::set_error(GPD_ERR_INVALID, "gzip-compressed capture: inflate it before indexing");
+  if (len < GPD_PCAP_HEADER_BYTES) return gpd::set_error(GPD_ERR_PCAP, "unexpected EOF");
+  uint32_t magic;
+  std::memcpy(&magic, buf, 4);  // binary.LittleEndian.Uint32(buf[0:4])
+  info->magic = magic;
+  if (magic == GPD_PCAP_MAGIC_NANO) {
+    info->big_endian = 0, info->nano = 1;
+  } else if (magic == GPD_PCAP_MAGIC_NANO_BE) {
+    info->big_endian = 1, info->nano = 1;
+  } else if (magic == GPD_PCAP_MAGIC_MICRO) {
+    info->big_endian = 0, info->nano = 0;
+  } else if (magic == GPD_PCAP_MAGIC_MICRO_BE) {
+    info->big_endian = 1, info->nano = 0;
+  } else {
+    return gpd::set_error(GPD_ERR_PCAP, "Unknown magic %x", magic);
+  }
+  const bool be = info->big_endian != 0;
+  info->version_major = gpd::rd16(buf + 4, be);
+  if (info->version_major != 2)
+    return gpd::set_error(GPD_ERR_PCAP, "Unknown major version %u", info->version_major);
+  info->version_minor = gpd::rd16(buf + 6, be);
+  if (info->version_minor != 4)
+    return gpd::set_error(GPD_ERR_PCAP, "Unknown minor version %u", info->version_minor);
+  info->snaplen = gpd::rd32(buf + 16, be);
+  info->linktype = gpd::rd32(buf + 20, be);
+  return GPD_OK;
+}
+
+int gpd_pcap_index(const uint8_t *buf, uint64_t len, const gpd_pcap_info *info, uint64_t pos,
+                   uint64_t max_n, uint32_t *offset, uint32_t *caplen, uint32_t *wirelen,
+                   uint64_t *ts_ns, uint64_t *n_out, uint64_t *next_pos, int *stop, int nthreads) {
+  if (!info || !n_out || (!buf && len) || (max_n && (!offset || !caplen)))
+    return gpd::set_error(GPD_ERR_INVALID, "gpd_pcap_index: null argument");
+  if (pos > len) return gpd::set_error(GPD_ERR_INVALID, "gpd_pcap_index: pos beyond the buffer");
+  gpd::PcapWalk W;
+  const int rc = gpd::pcap_walk(buf, len, *info, pos, max_n, nthreads, W);
+  if (W.n) {
+    const auto &last = W.plan.back();
+    if (W.R[last.r].pos[last.j0 + last.cnt - 1] + GPD_PCAP_RECORD_BYTES >= (1ull << 32))
+      return gpd::set_error(GPD_ERR_INVALID,
+                            "gpd_pcap_index: record offsets beyond 4 GiB; index the capture in windows");
+  }
+  gpd::pcap_emit(W, 0, offset, nullptr, caplen, wirelen, ts_ns);
+  *n_out = W.n;
+  if (next_pos) *next_pos = W.next_pos;
+  if (stop) *stop = W.stop;
+  return rc;
+}
+
+void gpd_pcap_last_stats(int *threads, int *met, int *rewalks) {
+  if (threads) *threads = gpd::g_last_threads;
+  if (met) *met = gpd::g_last_met;
+  if (rewalks) *rewalks = gpd::g_last_rewalks;
+}
+
+}  // extern "C"

@@ -14,6 +14,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <string>
+#include <thread>
 #include <vector>
 
 #include "gpd_internal.h"
@@ -29,6 +31,18 @@ int set_err(int code, const char *fmt, ...) {
   va_end(ap);
   return code;
 }
+
+}  // namespace
+
+int gpd::set_error(int code, const char *fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof g_err, fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+namespace {
 
 #define HIP_TRY(expr)                                                                    \
   do {                                                                                   \
@@ -214,6 +228,13 @@ struct gpd_ctx {
     bool busy = false;
   } slot[2];
   uint64_t slot_bytes = 0, slot_pkts = 0;
+  // host ranges pinned with gpd_host_register (H2D reads them in place)
+  std::vector<std::pair<const uint8_t *, uint64_t>> registered;
+  bool is_registered(const uint8_t *p, uint64_t n) const {
+    for (const auto &r : registered)
+      if (p >= r.first && p + n <= r.first + r.second) return true;
+    return false;
+  }
 };
 
 extern "C" {
@@ -346,6 +367,7 @@ int gpd_ctx_destroy(gpd_ctx *ctx) {
   if (ctx->d_pages) (void)hipFree(ctx->d_pages);
   for (auto &kv : ctx->fallback)
     if (kv.second.d) (void)hipFree(kv.second.d);
+  for (const auto &r : ctx->registered) (void)hipHostUnregister((void *)r.first);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   delete ctx;
@@ -594,6 +616,126 @@ int gpd_decode_host(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out) {
       drain_slot(s, out);
     }
   }
+  return GPD_OK;
+}
+
+// ---- pcap capture in host memory: index, then raw-byte chunks H2D -> decode -> D2H ----
+int gpd_host_register(gpd_ctx *ctx, const void *ptr, uint64_t len) {
+  if (!ctx || !ptr || !len) return set_err(GPD_ERR_INVALID, "gpd_host_register: bad argument");
+  HIP_TRY(hipSetDevice(ctx->device));
+  HIP_TRY(hipHostRegister(const_cast<void *>(ptr), len, hipHostRegisterDefault));
+  ctx->registered.emplace_back((const uint8_t *)ptr, len);
+  return GPD_OK;
+}
+
+int gpd_host_unregister(gpd_ctx *ctx, const void *ptr) {
+  if (!ctx) return set_err(GPD_ERR_INVALID, "gpd_host_unregister: null ctx");
+  for (size_t k = 0; k < ctx->registered.size(); k++) {
+    if (ctx->registered[k].first == ptr) {
+      HIP_TRY(hipSetDevice(ctx->device));
+      for (auto &s : ctx->slot)
+        if (s.stream) HIP_TRY(hipStreamSynchronize(s.stream));
+      HIP_TRY(hipHostUnregister(const_cast<void *>(ptr)));
+      ctx->registered.erase(ctx->registered.begin() + (long)k);
+      return GPD_OK;
+    }
+  }
+  return set_err(GPD_ERR_INVALID, "gpd_host_unregister: pointer not registered");
+}
+
+// memcpy split over threads (the staging copy of an unregistered capture)
+static void par_memcpy(uint8_t *dst, const uint8_t *src, uint64_t n, int nthreads) {
+  const uint64_t kMin = 8ull << 20;
+  int T = (int)std::min<uint64_t>((uint64_t)std::max(1, nthreads), std::max<uint64_t>(1, n / kMin));
+  if (T <= 1) {
+    std::memcpy(dst, src, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int k = 0; k < T; k++) {
+    const uint64_t lo = n * (uint64_t)k / (uint64_t)T, hi = n * (uint64_t)(k + 1) / (uint64_t)T;
+    th.emplace_back([=] { std::memcpy(dst + lo, src + lo, hi - lo); });
+  }
+  for (auto &t : th) t.join();
+}
+
+int gpd_decode_pcap(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, uint64_t max_n,
+                    const gpd_result *out, uint64_t *n_out, uint64_t *next_pos, int *stop,
+                    int nthreads) {
+  if (!ctx || !buf || !out || !out->status || !out->layers || !n_out)
+    return set_err(GPD_ERR_INVALID, "gpd_decode_pcap: null argument");
+  if (out->ext) return set_err(GPD_ERR_INVALID, "gpd_decode_pcap: ext records not supported");
+  if (nthreads <= 0) nthreads = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+  gpd_pcap_info info;
+  int rc = gpd_pcap_header(buf, len, &info);
+  if (rc) return rc;
+  gpd::PcapWalk W;
+  const int wrc = gpd::pcap_walk(buf, len, info, GPD_PCAP_HEADER_BYTES, max_n, nthreads, W);
+  std::string werr = wrc ? std::string(g_err) : std::string();
+  const uint64_t n = W.n;
+  std::vector<uint64_t> rp(n);
+  std::vector<uint32_t> rcap(n);
+  gpd::pcap_emit(W, 0, nullptr, rp.data(), rcap.data(), nullptr, nullptr);
+  *n_out = n;
+  if (next_pos) *next_pos = W.next_pos;
+  if (stop) *stop = W.stop;
+  W = gpd::PcapWalk{};  // free the walk
+  HIP_TRY(hipSetDevice(ctx->device));
+  const uint64_t kPkts = 1u << 20, kBytes = 256ull << 20;
+  rc = alloc_slots(ctx, kBytes, kPkts, false);
+  if (rc) return rc;
+  const bool pinned = ctx->is_registered(buf, len);
+  uint64_t i = 0;
+  int k = 0;
+  while (i < n) {
+    auto &s = ctx->slot[k];
+    if (s.busy) {
+      HIP_TRY(hipStreamSynchronize(s.stream));
+      drain_slot(s, out);
+    }
+    // records [i, j) whose bytes (from the first one's data, rounded down to 16) fit the slot
+    const uint64_t base = (rp[i] + GPD_PCAP_RECORD_BYTES) & ~15ull;
+    uint64_t j = i;
+    while (j < n && j - i < kPkts && rp[j] + GPD_PCAP_RECORD_BYTES + rcap[j] - base <= kBytes) j++;
+    if (j == i) return set_err(GPD_ERR_INVALID, "gpd_decode_pcap: record %llu larger than %llu bytes",
+                               (unsigned long long)i, (unsigned long long)kBytes);
+    const uint64_t m = j - i;
+    const uint64_t end = rp[j - 1] + GPD_PCAP_RECORD_BYTES + rcap[j - 1];
+    const uint64_t span = end - base;
+    for (uint64_t p = i; p < j; p++) {
+      s.h_off[p - i] = (uint32_t)(rp[p] + GPD_PCAP_RECORD_BYTES - base);
+      s.h_len[p - i] = rcap[p];
+    }
+    const uint8_t *src = buf + base;
+    if (!pinned) {
+      par_memcpy(s.h_data, src, span, nthreads);
+      src = s.h_data;
+    }
+    HIP_TRY(hipMemcpyAsync(s.d_data, src, span, hipMemcpyHostToDevice, s.stream));
+    HIP_TRY(hipMemcpyAsync(s.d_off, s.h_off, m * 4, hipMemcpyHostToDevice, s.stream));
+    HIP_TRY(hipMemcpyAsync(s.d_len, s.h_len, m * 4, hipMemcpyHostToDevice, s.stream));
+    gpd_batch b{s.d_data, span, s.d_off, s.d_len, m};
+    gpd_result r{s.d_status, s.d_layers, s.d_nh, s.d_th, s.d_csum, nullptr};
+    rc = launch(ctx, &b, &r, s.stream, false);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(s.h_status, s.d_status, m * 4, hipMemcpyDeviceToHost, s.stream));
+    HIP_TRY(hipMemcpyAsync(s.h_layers, s.d_layers, m * 8, hipMemcpyDeviceToHost, s.stream));
+    if (out->csum) HIP_TRY(hipMemcpyAsync(s.h_csum, s.d_csum, m * 4, hipMemcpyDeviceToHost, s.stream));
+    if (out->net_hash) HIP_TRY(hipMemcpyAsync(s.h_nh, s.d_nh, m * 8, hipMemcpyDeviceToHost, s.stream));
+    if (out->tp_hash) HIP_TRY(hipMemcpyAsync(s.h_th, s.d_th, m * 8, hipMemcpyDeviceToHost, s.stream));
+    s.lo = i;
+    s.hi = j;
+    s.busy = true;
+    i = j;
+    k ^= 1;
+  }
+  for (auto &s : ctx->slot) {
+    if (s.busy) {
+      HIP_TRY(hipStreamSynchronize(s.stream));
+      drain_slot(s, out);
+    }
+  }
+  if (wrc) return set_err(wrc, "%s", werr.c_str());
   return GPD_OK;
 }
 

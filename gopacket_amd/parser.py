@@ -22,8 +22,8 @@ from typing import Optional
 import numpy as np
 
 from . import layers as L
-from ._lib import GpdBatch, GpdConfig, GpdResult, check, lib
-from .batch import PacketBatch
+from ._lib import GPD_ERR_PCAP, GpdBatch, GpdConfig, GpdResult, check, lib
+from .batch import PAD, PacketBatch
 from .results import EXT_DTYPE, BatchResult
 
 DEC_ETHERNET, DEC_DOT1Q, DEC_IPV4, DEC_IPV6, DEC_IPV6_EXT = 1, 2, 4, 8, 16
@@ -255,6 +255,31 @@ class DecodingLayerParser:
                       res.ext.ctypes.data if ext else None)
         check(lib.gpd_decode_host(self.ctx().h, C.byref(b), C.byref(r)), "gpd_decode_host")
         return res
+
+    def DecodePcap(self, cap: np.ndarray, max_n: Optional[int] = None, nthreads: int = 0,
+                   data_len: Optional[int] = None):
+        """A whole in-memory capture (pcap.capture_array) through gpd_decode_pcap: records
+        indexed natively, their raw bytes chunked host -> device, decoded, results back.
+        Returns (BatchResult of the decoded records, number of records, error text or None —
+        the ReadPacketData loop's stop, pcapgo/read.go:120-137)."""
+        dl = cap.shape[0] - PAD if data_len is None else int(data_len)
+        m = (dl - 24) // 16 + 1 if max_n is None else int(max_n)
+        res = BatchResult(np.zeros(m, np.uint32), np.zeros(m, np.uint64), np.zeros(m, np.uint64),
+                          np.zeros(m, np.uint64), np.zeros(m, np.uint32), None)
+        r = GpdResult(res.status.ctypes.data, res.layers.ctypes.data, res.net_hash.ctypes.data,
+                      res.tp_hash.ctypes.data, res.csum.ctypes.data, None)
+        n, nxt, stop = C.c_uint64(), C.c_uint64(), C.c_int()
+        rc = lib.gpd_decode_pcap(self.ctx().h, cap.ctypes.data, dl, m, C.byref(r), C.byref(n),
+                                 C.byref(nxt), C.byref(stop), int(nthreads))
+        err = None
+        if rc == GPD_ERR_PCAP:
+            err = lib.gpd_last_error_string().decode()
+        elif rc != 0:
+            check(rc, "gpd_decode_pcap")
+        k = n.value
+        out = BatchResult(res.status[:k], res.layers[:k], res.net_hash[:k], res.tp_hash[:k],
+                          res.csum[:k], None)
+        return out, k, err
 
     def DecodeLayers(self, data: bytes, decoded: list):
         """parser.go:302-316 for one packet: fills `decoded`, sets self.Truncated, returns the

@@ -1,0 +1,113 @@
+/*
+ * gpd_pcap.h — C-ABI of the pcap ingest in front of the batched decoder.
+ *
+ * The reference reads a capture file one record at a time: pcapgo.NewReader parses the
+ * 24-byte file header and every ReadPacketData call parses one 16-byte record header and
+ * copies the record's bytes out (pcapgo/read.go:65-177).  Here a capture that is already in
+ * memory (a read or mmap'ed file) is indexed in one call — the record walk fills offset /
+ * caplen arrays that point INTO the capture buffer — and those arrays are exactly a
+ * gpd_batch over the capture bytes: nothing is repacked, and the raw capture bytes are what
+ * travel to HBM.
+ *
+ * Reference interfaces each entry point replaces (paths relative to google/gopacket):
+ *   gpd_pcap_header       pcapgo.NewReader / readHeader             pcapgo/read.go:65-117
+ *                         (Snaplen(), LinkType(), Resolution()       pcapgo/read.go:183-227)
+ *   gpd_pcap_index        the loop `for { data, ci, err := r.ReadPacketData() ... }` over a
+ *                         whole capture: ReadPacketData + readPacketHeader
+ *                                                                  pcapgo/read.go:120-177
+ *   gpd_decode_pcap       that loop feeding DecodingLayerParser.DecodeLayers
+ *                         (examples/statsassembly/main.go:171-177, pcap/gopacket_benchmark/
+ *                         benchmark.go:226-236): index + H2D of the raw capture bytes +
+ *                         gpd_decode + D2H, double-buffered
+ *   gpd_host_register     (no reference counterpart) pin a caller buffer so the H2D of
+ *                         gpd_decode_pcap reads it in place
+ *
+ * gzip-compressed captures (pcapgo/read.go:79-86) are inflated by the caller (the Python
+ * layer does it transparently); the walker sees uncompressed bytes.
+ */
+#ifndef GPD_PCAP_H_
+#define GPD_PCAP_H_
+#include "gpd.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* pcapgo magics (pcapgo/read.go:47-49, pcapgo/write.go:32) and version (write.go:33-34) */
+#define GPD_PCAP_MAGIC_MICRO     0xA1B2C3D4u
+#define GPD_PCAP_MAGIC_NANO      0xA1B23C4Du
+#define GPD_PCAP_MAGIC_MICRO_BE  0xD4C3B2A1u
+#define GPD_PCAP_MAGIC_NANO_BE   0x4D3CB2A1u
+#define GPD_PCAP_HEADER_BYTES    24
+#define GPD_PCAP_RECORD_BYTES    16
+
+/* Error returned when the walk stops at a record the reference would reject; the reference's
+ * error text is in gpd_last_error_string(). */
+#define GPD_ERR_PCAP (-5)
+
+/* Why a walk ended (gpd_pcap_index *stop). */
+#define GPD_PCAP_STOP_LIMIT     0  /* max_n records were returned; more may follow at *next_pos */
+#define GPD_PCAP_STOP_EOF       1  /* clean end: no bytes left where a record header would start (io.EOF) */
+#define GPD_PCAP_STOP_SHORT_HDR 2  /* 1..15 bytes left for a record header: "unexpected EOF" */
+#define GPD_PCAP_STOP_SNAPLEN   3  /* "capture length exceeds snap length: %d > %d" (read.go:125-127) */
+#define GPD_PCAP_STOP_ORIGLEN   4  /* "capture length exceeds original packet length: %d > %d" (read.go:129-131) */
+#define GPD_PCAP_STOP_SHORT_DATA 5 /* record data cut short: "unexpected EOF" ("EOF" when no byte is left) */
+
+typedef struct gpd_pcap_info {
+  uint32_t magic;          /* as read little-endian from bytes 0..3 */
+  uint32_t big_endian;     /* byte order of every header field */
+  uint32_t nano;           /* 1: nanosecond timestamps (nanoSecsFactor 1), 0: microseconds (1000) */
+  uint32_t version_major;  /* 2 */
+  uint32_t version_minor;  /* 4 */
+  uint32_t snaplen;        /* Snaplen() */
+  uint32_t linktype;       /* LinkType() (1 = Ethernet) */
+  uint32_t reserved;
+} gpd_pcap_info;
+
+/* readHeader (pcapgo/read.go:78-117) on buf[0:len): GPD_OK, or GPD_ERR_PCAP with the reference's
+ * text ("EOF", "unexpected EOF", "Unknown magic %x", "Unknown major version %d", "Unknown minor
+ * version %d").  A gzip magic (1f 8b) is reported as GPD_ERR_INVALID: inflate it first. */
+int gpd_pcap_header(const uint8_t *buf, uint64_t len, gpd_pcap_info *info);
+
+/* Walk the records of buf[pos:len) as successive ReadPacketData calls would (pcapgo/read.go:
+ * 120-137,165-177; pos = 24 for a whole file).  Record i of the walk is returned as
+ *   offset[i]  byte offset of its data in buf (record header + 16); < 2^32, so index captures
+ *              of more than 4 GiB in windows (pass buf = file + window base)
+ *   caplen[i]  CaptureInfo.CaptureLength, wirelen[i] CaptureInfo.Length (may be NULL)
+ *   ts_ns[i]   CaptureInfo.Timestamp as Unix nanoseconds, with the reference's uint32
+ *              product usec * nanoSecsFactor (read.go:172) (may be NULL)
+ * The walk stops after max_n records (*stop = LIMIT, *next_pos = where the next record header
+ * starts), at the clean end of the data (EOF), or at the first record the reference rejects:
+ * then *n_out counts the records before it, *next_pos is its header position and the call
+ * returns GPD_ERR_PCAP with the reference's error text.  nthreads > 1 walks segments of the
+ * buffer speculatively in parallel and stitches them where the true walk meets them; the
+ * result is identical to the sequential walk for every input (a segment whose speculation
+ * never meets the true walk is re-walked sequentially).  nthreads <= 0: the machine's cores,
+ * at most 16. */
+int gpd_pcap_index(const uint8_t *buf, uint64_t len, const gpd_pcap_info *info, uint64_t pos,
+                   uint64_t max_n, uint32_t *offset, uint32_t *caplen, uint32_t *wirelen,
+                   uint64_t *ts_ns, uint64_t *n_out, uint64_t *next_pos, int *stop, int nthreads);
+
+/* Index + decode a whole in-memory capture with the context's parser: the records are indexed
+ * (as gpd_pcap_index, nthreads as there), then decoded in chunks — the raw bytes of each chunk
+ * of records are copied host -> device as they lie in the capture (through pinned staging, or
+ * directly when buf lies in memory registered with gpd_host_register), decoded, and the
+ * results copied back — with two chunks in flight.  `out` holds host arrays of max_n entries
+ * (status and layers required, the rest optional; ext not supported).  Returns like
+ * gpd_pcap_index: the records before a rejected one are decoded and counted in *n_out. */
+int gpd_decode_pcap(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, uint64_t max_n,
+                    const gpd_result *out, uint64_t *n_out, uint64_t *next_pos, int *stop,
+                    int nthreads);
+
+/* Diagnostics of this thread's last walk: segments walked in parallel, segments whose
+ * speculation the true walk met, segments re-walked sequentially. */
+void gpd_pcap_last_stats(int *threads, int *met, int *rewalks);
+
+/* Pin / unpin host memory for in-place H2D (hipHostRegister on the context's device). */
+int gpd_host_register(gpd_ctx *ctx, const void *ptr, uint64_t len);
+int gpd_host_unregister(gpd_ctx *ctx, const void *ptr);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPD_PCAP_H_ */

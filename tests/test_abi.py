@@ -12,11 +12,11 @@ import pytest
 
 from conftest import ROOT, gpu_available
 
-HEADER = os.path.join(ROOT, "include", "gpd.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("gpd.h", "gpd_pcap.h")]
 
 
 def declared_functions():
-    src = open(HEADER).read()
+    src = "".join(open(h).read() for h in HEADERS)
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(gpd_[a-z0-9_]+)\s*\(", src)) -
                   {n for n in re.findall(r"#define\s+(gpd_\w+)", src)})
@@ -25,7 +25,8 @@ def declared_functions():
 def test_header_declares_the_boundary():
     fns = declared_functions()
     for f in ("gpd_ctx_create", "gpd_decode", "gpd_decode_host", "gpd_sync", "gpd_ctx_destroy",
-              "gpd_last_error_string", "gpd_ctx_reload_tables", "gpd_default_tables"):
+              "gpd_last_error_string", "gpd_ctx_reload_tables", "gpd_default_tables",
+              "gpd_pcap_header", "gpd_pcap_index", "gpd_decode_pcap", "gpd_host_register"):
         assert f in fns
 
 
@@ -58,15 +59,15 @@ def test_struct_layouts_match_c(tmp_path):
     from gopacket_amd import _lib
     from gopacket_amd.results import EXT_DTYPE
     prog = tmp_path / "sz.c"
-    prog.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "gpd.h"\nint main(void){'
-                    'printf("%zu %zu %zu %zu %zu %zu\\n", sizeof(gpd_config), sizeof(gpd_batch),'
+    prog.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "gpd_pcap.h"\nint main(void){'
+                    'printf("%zu %zu %zu %zu %zu %zu %zu\\n", sizeof(gpd_config), sizeof(gpd_batch),'
                     ' sizeof(gpd_result), sizeof(gpd_ext_rec), offsetof(gpd_ext_rec, obj),'
-                    ' sizeof(gpd_layer_rec)); return 0;}\n')
+                    ' sizeof(gpd_layer_rec), sizeof(gpd_pcap_info)); return 0;}\n')
     exe = tmp_path / "sz"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(prog), "-o", str(exe)], check=True)
     out = list(map(int, subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()))
     assert out == [C.sizeof(_lib.GpdConfig), C.sizeof(_lib.GpdBatch), C.sizeof(_lib.GpdResult),
-                   EXT_DTYPE.itemsize, EXT_DTYPE.fields["obj"][1], 16]
+                   EXT_DTYPE.itemsize, EXT_DTYPE.fields["obj"][1], 16, C.sizeof(_lib.GpdPcapInfo)]
 
 
 @pytest.mark.skipif(gpu_available(), reason="checks the no-device error path")
