@@ -42,6 +42,8 @@ const (
 	DecVXLAN      = C.GPD_DEC_VXLAN
 	DecPayload    = C.GPD_DEC_PAYLOAD
 	DecFragment   = C.GPD_DEC_FRAGMENT
+	DecICMPv4     = C.GPD_DEC_ICMPV4
+	DecLLC        = C.GPD_DEC_LLC
 	DecAll        = C.GPD_DEC_ALL
 	optIgnoreUnsp = C.GPD_OPT_IGNORE_UNSUPPORTED
 	optIgnorePan  = C.GPD_OPT_IGNORE_PANIC
@@ -71,6 +73,10 @@ func decoderBit(d gopacket.DecodingLayer) (uint32, error) {
 		return DecPayload, nil
 	case *gopacket.Fragment:
 		return DecFragment, nil
+	case *layers.ICMPv4:
+		return DecICMPv4, nil
+	case *layers.LLC:
+		return DecLLC, nil
 	}
 	return 0, fmt.Errorf("gpdecode: %T has no MI355X decoder", d)
 }
@@ -251,7 +257,7 @@ var codeLayerType = [16]gopacket.LayerType{0, layers.LayerTypeEthernet, layers.L
 	layers.LayerTypeIPv4, layers.LayerTypeIPv6, layers.LayerTypeIPv6HopByHop,
 	layers.LayerTypeIPv6Routing, layers.LayerTypeIPv6Fragment, layers.LayerTypeIPv6Destination,
 	layers.LayerTypeTCP, layers.LayerTypeUDP, layers.LayerTypeVXLAN,
-	gopacket.LayerTypePayload, gopacket.LayerTypeFragment, 0, 0}
+	gopacket.LayerTypePayload, gopacket.LayerTypeFragment, layers.LayerTypeICMPv4, layers.LayerTypeLLC}
 
 // Decoded fills decoded exactly as DecodeLayers would (parser.go:302-316).
 func (r *Result) Decoded(i int, decoded *[]gopacket.LayerType) {
@@ -301,6 +307,7 @@ var errorText = map[uint32]string{
 	18: "IPv6 has jumbo length and IPv6 length is not 0",
 	19: "IPv6 length 0, but HopByHop header does not have jumbogram option",
 	23: "TCP data offset greater than packet length", 29: "vxlan packet too small",
+	30: "ICMP layer less then 8 bytes for ICMPv4 packet", 31: "LLC header too small",
 }
 
 func lastError(what string, rc C.int) error {

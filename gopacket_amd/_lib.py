@@ -11,7 +11,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GPD_LIB_PATH") or os.path.join(_HERE, "libgpd.so")  # override: A/B only
 
-GPD_ABI_VERSION = 1
+GPD_ABI_VERSION = 2
 GPD_OK = 0
 
 

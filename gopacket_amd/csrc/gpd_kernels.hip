@@ -131,7 +131,8 @@ __device__ __forceinline__ uint32_t be16_at(const uint32_t (&w)[N], int o) {
 
 // ---------------------------------------------------------------- tables
 enum Dec : uint32_t {
-  D_ETH, D_DOT1Q, D_IP4, D_IP6, D_IP6EXT, D_TCP, D_UDP, D_VXLAN, D_PAYLOAD, D_FRAG, D_NONE = 15
+  D_ETH, D_DOT1Q, D_IP4, D_IP6, D_IP6EXT, D_TCP, D_UDP, D_VXLAN, D_PAYLOAD, D_FRAG, D_ICMP4,
+  D_LLC, D_NONE = 15
 };
 
 struct TE {        // a dispatch-table result
@@ -446,6 +447,26 @@ __device__ __forceinline__ Out decode_packet(const S &s, uint32_t caplen, const 
           if (len < 8) GPD_FAIL(GPD_E_VXLAN_TOO_SMALL, 0, 0);
           c_len = 8; p_off = off + 8; p_len = len - 8;
           next = GPD_LT_ETHERNET;
+          break;
+        }
+        case D_ICMP4: {  // icmp4.go:220-231; NextLayerType :261-263
+          if (len < 8) { truncated = 1; GPD_FAIL(GPD_E_ICMP4_TOO_SMALL, 0, 0); }
+          c_len = 8; p_off = off + 8; p_len = len - 8;
+          next = GPD_LT_PAYLOAD;
+          break;
+        }
+        case D_LLC: {  // llc.go:31-52; NextLayerType :61-69
+          if (len < 3) GPD_FAIL(GPD_E_LLC_TOO_SMALL, 0, 0);
+          const uint32_t dsap = s.u8(off) & 0xFEu, ssap = s.u8(off + 1) & 0xFEu;
+          const uint32_t ctl = s.u8(off + 2);
+          c_len = 3;
+          if (!(ctl & 1u) || (ctl & 3u) == 1u) {  // two-byte control field
+            if (len < 4) GPD_FAIL(GPD_E_LLC_TOO_SMALL, 0, 0);
+            c_len = 4;
+          }
+          p_off = off + c_len; p_len = len - c_len;
+          next = (dsap == 0xAAu && ssap == 0xAAu) ? (uint32_t)GPD_LT_SNAP
+               : (dsap == 0x42u && ssap == 0x42u) ? (uint32_t)GPD_LT_STP : (uint32_t)GPD_LT_ZERO;
           break;
         }
         default: {  // Payload / Fragment: all of it; LayerPayload nil; next Zero

@@ -109,7 +109,7 @@ void type_lut(uint32_t decoders, uint8_t lut[128]) {
   struct E { uint32_t lt, dec, code; };
   static const E kMap[] = {{17, 0, 1},  {15, 1, 2},  {20, 2, 3},  {21, 3, 4},  {46, 4, 5},
                            {47, 4, 6},  {48, 4, 7},  {49, 4, 8},  {44, 5, 9},  {45, 6, 10},
-                           {116, 7, 11}, {2, 8, 12}, {3, 9, 13}};
+                           {116, 7, 11}, {2, 8, 12}, {3, 9, 13}, {19, 10, 14}, {22, 11, 15}};
   memset(lut, 0xFF, 128);
   for (const E &e : kMap)
     if (decoders & (1u << e.dec)) lut[e.lt] = (uint8_t)(e.dec | (e.code << 4));

@@ -39,6 +39,8 @@ _FORMATS = {
     27: "Invalid UDP header. Length {0} less than 8",
     28: "UDP packet too small: {0} bytes",
     29: "vxlan packet too small",
+    30: "ICMP layer less then 8 bytes for ICMPv4 packet",
+    31: "LLC header too small",
 }
 
 ERR_CODE_NAMES = {
@@ -49,7 +51,7 @@ ERR_CODE_NAMES = {
     17: "IP6_JUMBO_TOO_SMALL", 18: "IP6_JUMBO_AND_LEN", 19: "IP6_LEN0_NO_JUMBO",
     20: "IP6_LEN0_NOT_HBH", 21: "TCP_TOO_SHORT", 22: "TCP_DOFF_LT5", 23: "TCP_DOFF_GT_LEN",
     24: "TCP_OPT_LT2_REM", 25: "TCP_OPT_LEN_LT2", 26: "TCP_OPT_EXCEEDS", 27: "UDP_TOO_SHORT",
-    28: "UDP_LEN_TOO_SMALL", 29: "VXLAN_TOO_SMALL",
+    28: "UDP_LEN_TOO_SMALL", 29: "VXLAN_TOO_SMALL", 30: "ICMP4_TOO_SMALL", 31: "LLC_TOO_SMALL",
 }
 
 

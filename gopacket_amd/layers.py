@@ -33,6 +33,7 @@ LayerTypeICMPv4 = 19
 LayerTypeIPv4 = 20
 LayerTypeIPv6 = 21
 LayerTypeLLC = 22
+LayerTypeSNAP = 23
 LayerTypeMPLS = 24
 LayerTypePPP = 25
 LayerTypePPPoE = 26
@@ -59,6 +60,7 @@ LayerTypeNTP = 117
 LayerTypeDHCPv4 = 118
 LayerTypeVRRP = 119
 LayerTypeGeneve = 120
+LayerTypeSTP = 121
 LayerTypeBFD = 122
 LayerTypeOSPF = 123
 LayerTypeGTPv1U = 129
@@ -87,7 +89,7 @@ EndpointUDPPort = 5
 CODE_TO_LAYERTYPE = (0, LayerTypeEthernet, LayerTypeDot1Q, LayerTypeIPv4, LayerTypeIPv6,
                      LayerTypeIPv6HopByHop, LayerTypeIPv6Routing, LayerTypeIPv6Fragment,
                      LayerTypeIPv6Destination, LayerTypeTCP, LayerTypeUDP, LayerTypeVXLAN,
-                     LayerTypePayload, LayerTypeFragment, 0, 0)
+                     LayerTypePayload, LayerTypeFragment, LayerTypeICMPv4, LayerTypeLLC)
 LAYERTYPE_TO_CODE = {lt: c for c, lt in enumerate(CODE_TO_LAYERTYPE) if lt}
 
 

@@ -28,6 +28,7 @@ from .results import EXT_DTYPE, BatchResult
 
 DEC_ETHERNET, DEC_DOT1Q, DEC_IPV4, DEC_IPV6, DEC_IPV6_EXT = 1, 2, 4, 8, 16
 DEC_TCP, DEC_UDP, DEC_VXLAN, DEC_PAYLOAD, DEC_FRAGMENT = 32, 64, 128, 256, 512
+DEC_ICMPV4, DEC_LLC = 1024, 2048
 OPT_IGNORE_UNSUPPORTED, OPT_IGNORE_PANIC = 1, 2
 OPT_NO_CHECKSUMS, OPT_NO_FLOW_HASH = 256, 512
 
@@ -81,8 +82,16 @@ class Fragment(DecodingLayer):      # base.go:111
     bit, can_decode = DEC_FRAGMENT, (L.LayerTypeFragment,)
 
 
+class ICMPv4(DecodingLayer):        # layers/icmp4.go:256-258
+    bit, can_decode = DEC_ICMPV4, (L.LayerTypeICMPv4,)
+
+
+class LLC(DecodingLayer):           # layers/llc.go:55-57
+    bit, can_decode = DEC_LLC, (L.LayerTypeLLC,)
+
+
 DECODER_BY_NAME = {c.__name__: c for c in (Ethernet, Dot1Q, IPv4, IPv6, IPv6ExtensionSkipper, TCP,
-                                            UDP, VXLAN, Payload, Fragment)}
+                                            UDP, VXLAN, Payload, Fragment, ICMPv4, LLC)}
 
 
 def decoder_mask(decoders) -> int:

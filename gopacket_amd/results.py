@@ -17,14 +17,14 @@ from .errors import DecodeError, UnsupportedLayerType
 from .layers import CODE_TO_LAYERTYPE
 
 OBJ_NAMES = ("Ethernet", "Dot1Q", "IPv4", "IPv6", "IPv6ExtensionSkipper", "TCP", "UDP", "VXLAN",
-             "Payload", "Fragment")
+             "Payload", "Fragment", "ICMPv4", "LLC")
 
 LAYER_REC_DTYPE = np.dtype([("contents_off", "<u4"), ("contents_len", "<u4"),
                             ("payload_off", "<u4"), ("payload_len", "<u4")])
 EXT_DTYPE = np.dtype([("layer_codes", "<u8", (2,)), ("err_arg0", "<u4"), ("err_arg1", "<u4"),
                       ("obj_valid", "<u2"), ("pad0", "<u2"), ("pad1", "<u4"),
-                      ("obj", LAYER_REC_DTYPE, (10,))])
-assert EXT_DTYPE.itemsize == 192
+                      ("obj", LAYER_REC_DTYPE, (12,))])
+assert EXT_DTYPE.itemsize == 224
 
 ST_OK, ST_UNSUPPORTED, ST_DECODE_ERROR = 0, 1, 2
 

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define GPD_ABI_VERSION 1
+#define GPD_ABI_VERSION 2  /* 2: ICMPv4 + LLC decoders, 12 objects, 224-B ext record */
 
 /* ---- gopacket LayerType numbers (layertypes.go:14-154, decode.go:105-116) ---- */
 #define GPD_LT_ZERO            0
@@ -54,6 +54,7 @@ extern "C" {
 #define GPD_LT_IPV4            20
 #define GPD_LT_IPV6            21
 #define GPD_LT_LLC             22
+#define GPD_LT_SNAP            23
 #define GPD_LT_TCP             44
 #define GPD_LT_UDP             45
 #define GPD_LT_IPV6_HOPBYHOP   46
@@ -63,6 +64,7 @@ extern "C" {
 #define GPD_LT_ICMPV6          57
 #define GPD_LT_DNS             107
 #define GPD_LT_VXLAN           116
+#define GPD_LT_STP             121
 #define GPD_LT_TLS             140
 
 /* ---- DecodingLayers this engine implements (bit = registered) ----
@@ -78,7 +80,9 @@ extern "C" {
 #define GPD_DEC_VXLAN      (1u << 7)  /* {116}           layers/vxlan.go:43-78            */
 #define GPD_DEC_PAYLOAD    (1u << 8)  /* {2}             gopacket.Payload base.go:55-63   */
 #define GPD_DEC_FRAGMENT   (1u << 9)  /* {3}             gopacket.Fragment base.go:108-117 */
-#define GPD_DEC_ALL        0x3FFu
+#define GPD_DEC_ICMPV4     (1u << 10) /* {19}            layers/icmp4.go:220-231,261-263  */
+#define GPD_DEC_LLC        (1u << 11) /* {22}            layers/llc.go:31-52,61-69        */
+#define GPD_DEC_ALL        0xFFFu
 
 /* ---- options (DecodingLayerParserOptions, parser.go:336-350, + engine knobs) ---- */
 #define GPD_OPT_IGNORE_UNSUPPORTED (1u << 0)  /* parser.IgnoreUnsupported = true */
@@ -140,7 +144,9 @@ extern "C" {
 #define GPD_C_VXLAN     11
 #define GPD_C_PAYLOAD   12
 #define GPD_C_FRAGMENT  13
-/* code -> LayerType: {0,17,15,20,21,46,47,48,49,44,45,116,2,3,0,0} */
+#define GPD_C_ICMPV4    14
+#define GPD_C_LLC       15
+/* code -> LayerType: {0,17,15,20,21,46,47,48,49,44,45,116,2,3,19,22} */
 
 /* ---- checksum word (uint32): [15:0] IPv4 header checksum as ip4.go:158 `checksum`
  *      computes it over ip4.Contents (compare with the stored field); [31:16] L4 checksum as
@@ -181,14 +187,17 @@ enum gpd_err {
   GPD_E_UDP_TOO_SHORT = 27,       /* udp.go:31-33       "Invalid UDP header. Length %d less than 8" */
   GPD_E_UDP_LEN_TOO_SMALL = 28,   /* udp.go:52-53       "UDP packet too small: %d bytes" */
   GPD_E_VXLAN_TOO_SMALL = 29,     /* vxlan.go:54-56     "vxlan packet too small" */
-  GPD_E_COUNT = 30
+  GPD_E_ICMP4_TOO_SMALL = 30,     /* icmp4.go:221-223   "ICMP layer less then 8 bytes for ICMPv4 packet" (sets Truncated) */
+  GPD_E_LLC_TOO_SMALL = 31,       /* llc.go:32-33,42-43 "LLC header too small" */
+  GPD_E_COUNT = 32
 };
 
 /* ---- layer objects: one per registered DecodingLayer (its state after the call) ---- */
 enum gpd_obj {
   GPD_OBJ_ETHERNET = 0, GPD_OBJ_DOT1Q = 1, GPD_OBJ_IPV4 = 2, GPD_OBJ_IPV6 = 3,
   GPD_OBJ_IPV6_EXT = 4, GPD_OBJ_TCP = 5, GPD_OBJ_UDP = 6, GPD_OBJ_VXLAN = 7,
-  GPD_OBJ_PAYLOAD = 8, GPD_OBJ_FRAGMENT = 9, GPD_NOBJ = 10
+  GPD_OBJ_PAYLOAD = 8, GPD_OBJ_FRAGMENT = 9, GPD_OBJ_ICMPV4 = 10, GPD_OBJ_LLC = 11,
+  GPD_NOBJ = 12
 };
 
 /* BaseLayer of one object after its last successful DecodeFromBytes in this packet:
@@ -198,7 +207,7 @@ typedef struct gpd_layer_rec {
   uint32_t contents_off, contents_len, payload_off, payload_len;
 } gpd_layer_rec;
 
-/* Optional extended record (192 B) — everything a Go/C++ shim needs to rebuild the
+/* Optional extended record (224 B) — everything a Go/C++ shim needs to rebuild the
  * decoded slice, the exact error text and every layer struct by reading header bytes. */
 typedef struct gpd_ext_rec {
   uint64_t layer_codes[2];  /* decoded[0..31] as 4-bit codes, decoded[i] at bit 4*(i%16) of word i/16 */

@@ -15,7 +15,8 @@
 
 typedef struct { uint32_t off, len; } sl; /* a Go []byte: pkt[off : off+len] */
 
-enum { D_ETH, D_DOT1Q, D_IP4, D_IP6, D_IP6EXT, D_TCP, D_UDP, D_VXLAN, D_PAYLOAD, D_FRAG };
+enum { D_ETH, D_DOT1Q, D_IP4, D_IP6, D_IP6EXT, D_TCP, D_UDP, D_VXLAN, D_PAYLOAD, D_FRAG, D_ICMP4,
+       D_LLC };
 
 typedef struct {
   const uint8_t *pkt;
@@ -260,6 +261,33 @@ static int dec_vxlan(st *s, sl d) {
   return 0;
 }
 
+/* ICMPv4.DecodeFromBytes, layers/icmp4.go:220-231; NextLayerType :261-263 (always Payload) */
+static int dec_icmp4(st *s, sl d) {
+  if (d.len < 8) { s->truncated = 1; return fail(s, GPD_E_ICMP4_TOO_SMALL, 0, 0); }
+  s->contents = (sl){d.off, 8};
+  s->payload = (sl){d.off + 8, d.len - 8};
+  s->next = GPD_LT_PAYLOAD;
+  return 0;
+}
+
+/* LLC.DecodeFromBytes, layers/llc.go:31-52; NextLayerType :61-69 */
+static int dec_llc(st *s, sl d) {
+  const uint8_t *p = s->pkt + d.off;
+  if (d.len < 3) return fail(s, GPD_E_LLC_TOO_SMALL, 0, 0);
+  uint32_t dsap = p[0] & 0xFE, ssap = p[1] & 0xFE, control = p[2];
+  uint32_t hl = 3;
+  if ((control & 0x1) == 0 || (control & 0x3) == 0x1) {
+    if (d.len < 4) return fail(s, GPD_E_LLC_TOO_SMALL, 0, 0);
+    hl = 4;
+  }
+  s->contents = (sl){d.off, hl};
+  s->payload = (sl){d.off + hl, d.len - hl};
+  if (dsap == 0xAA && ssap == 0xAA) s->next = GPD_LT_SNAP;
+  else if (dsap == 0x42 && ssap == 0x42) s->next = GPD_LT_STP;
+  else s->next = GPD_LT_ZERO;
+  return 0;
+}
+
 /* Payload / Fragment DecodeFromBytes, base.go:60-63,115-117: the whole data; LayerPayload
  * is nil and NextLayerType is Zero, base.go:42,57,99,112 */
 static int dec_rest(st *s, sl d) {
@@ -285,6 +313,8 @@ static int lookup(uint32_t typ, uint32_t mask) {
     case GPD_LT_VXLAN: return (mask & GPD_DEC_VXLAN) ? D_VXLAN : -1;
     case GPD_LT_PAYLOAD: return (mask & GPD_DEC_PAYLOAD) ? D_PAYLOAD : -1;
     case GPD_LT_FRAGMENT: return (mask & GPD_DEC_FRAGMENT) ? D_FRAG : -1;
+    case GPD_LT_ICMPV4: return (mask & GPD_DEC_ICMPV4) ? D_ICMP4 : -1;
+    case GPD_LT_LLC: return (mask & GPD_DEC_LLC) ? D_LLC : -1;
     default: return -1;
   }
 }
@@ -304,13 +334,15 @@ static uint32_t code_of(uint32_t typ) {
     case GPD_LT_VXLAN: return GPD_C_VXLAN;
     case GPD_LT_PAYLOAD: return GPD_C_PAYLOAD;
     case GPD_LT_FRAGMENT: return GPD_C_FRAGMENT;
+    case GPD_LT_ICMPV4: return GPD_C_ICMPV4;
+    case GPD_LT_LLC: return GPD_C_LLC;
     default: return GPD_C_NONE;
   }
 }
 
 static const int obj_of_dec[] = {GPD_OBJ_ETHERNET, GPD_OBJ_DOT1Q, GPD_OBJ_IPV4, GPD_OBJ_IPV6,
                                  GPD_OBJ_IPV6_EXT, GPD_OBJ_TCP, GPD_OBJ_UDP, GPD_OBJ_VXLAN,
-                                 GPD_OBJ_PAYLOAD, GPD_OBJ_FRAGMENT};
+                                 GPD_OBJ_PAYLOAD, GPD_OBJ_FRAGMENT, GPD_OBJ_ICMPV4, GPD_OBJ_LLC};
 
 /* ip4.go:158-179 `checksum`: bytes 10-11 read as zero, fold `for csum > 0xffff`, invert. */
 uint16_t gpo_ip4_header_checksum(const uint8_t *b, uint32_t len) {
@@ -420,6 +452,8 @@ void gpo_decode_packet(const uint8_t *pkt, uint32_t caplen, uint32_t first, uint
         case D_TCP: rc = dec_tcp(&s, data); break;
         case D_UDP: rc = dec_udp(&s, data); break;
         case D_VXLAN: rc = dec_vxlan(&s, data); break;
+        case D_ICMP4: rc = dec_icmp4(&s, data); break;
+        case D_LLC: rc = dec_llc(&s, data); break;
         default: rc = dec_rest(&s, data); break;
       }
       if (rc) { klass = GPD_ST_DECODE_ERROR; break; }

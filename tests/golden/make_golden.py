@@ -278,6 +278,53 @@ case("udp6_dstopts_checksum_kat", v6 + dst + udp,
      "layers/tcpip_test.go:17,95-137 (Wireshark-confirmed 0x4d21; DstOpts with one PadN(4) option)",
      first="IPv6")
 
+# 15. ICMPv4 and LLC decoders
+p = go_bytes_at("layers/vxlan_test.go", "var testPacketVXLAN")
+src = f"layers/vxlan_test.go:{line_of('layers/vxlan_test.go', 'var testPacketVXLAN')}"
+case("vxlan_icmp_full", p, src, ["Ethernet", "IPv4", "UDP", "VXLAN", "ICMPv4", "Payload"],
+     {"decoded": ["Ethernet", "IPv4", "UDP", "VXLAN", "Ethernet", "IPv4", "ICMPv4", "Payload"],
+      "err": None, "truncated": False,
+      "vxlan": {"contents": [42, 50], "VNI": 255, "ValidIDFlag": True},
+      "icmpv4": {"contents": [84, 92], "payload": [92, len(p)], "Type": 8, "Code": 0},
+      "inner_ipv4_contents": [64, 84]},
+     "layers/vxlan_test.go:53-80 (checkLayers [Ethernet IPv4 UDP VXLAN Ethernet IPv4 ICMPv4 "
+     "Payload], VNI 255, I flag); the inner IPv4 stays in the reused ip4 object (A11)")
+p = go_bytes_at("layers/decode_test.go", "var testICMP = ")
+src = f"layers/decode_test.go:{line_of('layers/decode_test.go', 'var testICMP = ')}"
+case("icmp4_unreachable", p, src, ["Ethernet", "IPv4", "ICMPv4", "TCP", "UDP", "Payload"],
+     {"decoded": ["Ethernet", "IPv4", "ICMPv4", "Payload"], "err": None, "truncated": False,
+      "ip4_csum": 0xD7A7,
+      "icmpv4": {"contents": [34, 42], "payload": [42, 70], "Type": 3, "Code": 13,
+                 "Checksum": 0x946E, "Id": 0, "Seq": 0}},
+     "layers/decode_test.go:1094-1100 (checkLayers [Ethernet IPv4 ICMPv4 Payload]; "
+     "testSerialization re-creates the bytes, pinning the IPv4 checksum 0xd7a7); icmp4.go:220-231 "
+     "fields")
+case("icmp4_truncated", p[:14 + 20 + 5], src, ["Ethernet", "IPv4", "ICMPv4", "Payload"],
+     {"decoded": ["Ethernet", "IPv4"], "err": "ICMP layer less then 8 bytes for ICMPv4 packet",
+      "truncated": True},
+     "derived: ip4.go:228-230 (Length 56 > 25 captured: Truncated), icmp4.go:221-223 (< 8 bytes: "
+     "SetTruncated + error)")
+p = go_bytes_at("layers/decode_test.go", "testSTPpacket := ")
+src = f"layers/decode_test.go:{line_of('layers/decode_test.go', 'testSTPpacket := ')}"
+case("stp_llc", p, src, ["Ethernet", "LLC", "Payload"],
+     {"decoded": ["Ethernet", "LLC"], "err": "No decoder for layer type STP", "stop": 121,
+      "truncated": False,
+      "llc": {"contents": [14, 17], "payload": [17, 52], "DSAP": 0x42, "SSAP": 0x42, "Control": 3}},
+     "layers/decode_test.go:1376-1380 (checkLayers [Ethernet LLC STP]); ethernet.go:50-57 trims the "
+     "payload to the 802.3 length 38; llc.go:40-50 one-byte control; STP is not registered in "
+     "this DLP (parser.go:308-314)")
+case("stp_llc_ignore", p, src, ["Ethernet", "LLC", "Payload"],
+     {"decoded": ["Ethernet", "LLC"], "err": None, "stop": 121, "truncated": False},
+     "as stp_llc with IgnoreUnsupported (parser.go:310-312)", ignore_unsupported=True)
+p = go_bytes_at("layers/decode_test.go", "func TestDecodeNortelDiscovery")
+src = f"layers/decode_test.go:{line_of('layers/decode_test.go', 'func TestDecodeNortelDiscovery')}"
+case("nortel_llc_snap", p, src, ["Ethernet", "LLC", "Payload"],
+     {"decoded": ["Ethernet", "LLC"], "err": "No decoder for layer type SNAP", "stop": 23,
+      "truncated": False,
+      "llc": {"contents": [14, 17], "payload": [17, 33], "DSAP": 0xAA, "SSAP": 0xAA, "Control": 3}},
+     "layers/decode_test.go:970-974 (checkLayers [Ethernet LLC SNAP NortelDiscovery]); the DLP "
+     "has no SNAP decoder, so it stops there (parser.go:308-314)")
+
 # 14. pcap fixtures
 for fn in ("test_ethernet.pcap", "test_dns.pcap"):
     shutil.copyfile(os.path.join(REF, "pcap", fn), os.path.join(OUT, fn))

@@ -16,7 +16,7 @@ GOLDEN = os.path.join(HERE, "golden", "golden.json")
 
 NAME_TO_LT = {v: k for k, v in LAYERTYPE_NAMES.items()}
 DEC_BITS = {"Ethernet": 1, "Dot1Q": 2, "IPv4": 4, "IPv6": 8, "IPv6ExtensionSkipper": 16, "TCP": 32,
-            "UDP": 64, "VXLAN": 128, "Payload": 256, "Fragment": 512}
+            "UDP": 64, "VXLAN": 128, "Payload": 256, "Fragment": 512, "ICMPv4": 1024, "LLC": 2048}
 
 
 def load():
@@ -141,6 +141,21 @@ def check(c, res, i: int = 0, pkt: bytes | None = None) -> None:
             assert h[0] >> 5 == f["Priority"] and bool(h[0] & 0x10) == f["DropEligible"]
         if obj == "VXLAN":
             assert int.from_bytes(h[4:7], "big") == f["VNI"] and bool(h[0] & 0x08) == f["ValidIDFlag"]
+    if "icmpv4" in e and res.ext is not None:  # icmp4.go:220-231
+        (c0, c1), (p0, p1) = res.layer(i, "ICMPv4")
+        f = e["icmpv4"]
+        assert [c0, c1] == f["contents"] and [p0, p1] == f["payload"], f"{name}: ICMPv4 {(c0, c1)}"
+        h = pkt[c0:c1]
+        assert (h[0], h[1]) == (f["Type"], f["Code"]), f"{name}: ICMPv4 TypeCode"
+        if "Checksum" in f:
+            assert struct.unpack(">HHH", h[2:8]) == (f["Checksum"], f["Id"], f["Seq"])
+    if "llc" in e and res.ext is not None:  # llc.go:31-52
+        (c0, c1), (p0, p1) = res.layer(i, "LLC")
+        f = e["llc"]
+        assert [c0, c1] == f["contents"] and [p0, p1] == f["payload"], f"{name}: LLC {(c0, c1)}"
+        h = pkt[c0:c1]
+        ctl = h[2] if c1 - c0 == 3 else (h[2] << 8) | h[3]
+        assert (h[0] & 0xFE, h[1] & 0xFE, ctl) == (f["DSAP"], f["SSAP"], f["Control"])
     if "inner_ipv4_contents" in e and res.ext is not None:
         (c0, c1), _ = res.layer(i, "IPv4")
         assert [c0, c1] == e["inner_ipv4_contents"], f"{name}: A11 inner IPv4 {(c0, c1)}"

@@ -18,7 +18,7 @@ from gopacket_amd.batch import PacketBatch
 
 pytestmark = pytest.mark.gpu
 
-ALL = 0x3FF
+ALL = 0xFFF  # every decoder, ICMPv4 and LLC included (gpd.h GPD_DEC_ALL)
 
 
 def _parser(first=L.LayerTypeEthernet, mask=ALL, options=0, tables=None):
@@ -78,8 +78,10 @@ def _golden_packets():
 
 @pytest.mark.parametrize("first", [L.LayerTypeEthernet, L.LayerTypeIPv4, L.LayerTypeIPv6,
                                    L.LayerTypeTCP, L.LayerTypeDot1Q, 999])
-@pytest.mark.parametrize("mask", [ALL, 0x1 | 0x4 | 0x20 | 0x100, 0x1 | 0x2 | 0x4 | 0x40 | 0x80,
-                                  0x1 | 0x8 | 0x10 | 0x40 | 0x200])
+@pytest.mark.parametrize("mask", [ALL, 0x3FF, 0x1 | 0x4 | 0x20 | 0x100, 0x1 | 0x2 | 0x4 | 0x40 | 0x80,
+                                  0x1 | 0x8 | 0x10 | 0x40 | 0x200,
+                                  0x1 | 0x4 | 0x400 | 0x20 | 0x40 | 0x100,  # benchmark.go:216-218
+                                  0x1 | 0x800 | 0x100])
 def test_golden_batch_configs(first, mask):
     run_both(PacketBatch.from_packets(_golden_packets()), first, mask, 0)
     run_both(PacketBatch.from_packets(_golden_packets()), first, mask, 1)
@@ -108,6 +110,7 @@ def test_fuzz_truncations_and_mutations(options):
     pk = _mutations()
     b = PacketBatch.from_packets(pk)
     run_both(b, L.LayerTypeEthernet, ALL, options)
+    run_both(b, L.LayerTypeEthernet, 0x3FF, options)
     run_both(b, L.LayerTypeIPv4, 0x4 | 0x20 | 0x40 | 0x100, options)
 
 
