@@ -76,6 +76,15 @@ def _load():
         raise ImportError(
             f"gopacket_amd: native library {LIB_PATH} is missing — build it with "
             "`python -m gopacket_amd.build` (hipcc, gfx950); there is no CPU fallback")
+    # One HIP runtime per process.  PyTorch ships its own libamdhip64 / libhsa-runtime64 and
+    # its extension modules NEED them under a different name than libgpd.so does
+    # (libamdhip64.so vs .so.7), so loading libgpd.so first would bring up a second runtime,
+    # which finds no device once torch's has opened it.  Loading torch first makes libgpd.so
+    # bind to torch's (same SONAME).  Without torch (a C or Go host) libgpd.so uses /opt/rocm's.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(LIB_PATH)
     for name, (res, args) in EXPORTS.items():
         fn = getattr(lib, name)

@@ -2,6 +2,7 @@
 
   gopacket_amd/libgpd.so       product: HIP kernels (gfx950) + C-ABI runtime (include/gpd.h)
   oracle/libgpd_oracle.so      test infrastructure: CPU restatement (oracle/)
+  tests/c/abi_host             test driver: a plain C host on the C-ABI (no Python/torch)
 
 Both are built with plain compiler invocations (hipcc / gcc); no cmake.  The .so
 files are git-ignored and travel to the GPU box with the repository snapshot.
@@ -55,7 +56,25 @@ def build_oracle(force: bool = False) -> str:
     return ORACLE_LIB
 
 
+ABI_HOST = os.path.join(ROOT, "tests", "c", "abi_host")
+
+
+def build_abi_host(force: bool = False) -> str:
+    """tests/c/abi_host: links libgpd.so (rpath to the in-tree copy) and the oracle."""
+    src = os.path.join(ROOT, "tests", "c", "abi_host.c")
+    deps = [src, LIB, ORACLE_LIB, os.path.join(ROOT, "include", "gpd.h")]
+    if force or _stale(ABI_HOST, deps):
+        subprocess.run(["gcc", "-O2", "-std=c11", "-Wall", "-D__HIP_PLATFORM_AMD__",
+                        "-I/opt/rocm/include", src, "-o", ABI_HOST,
+                        "-L" + PKG, "-lgpd", "-L" + os.path.dirname(ORACLE_LIB), "-lgpd_oracle",
+                        "-L/opt/rocm/lib", "-lamdhip64",
+                        "-Wl,-rpath,$ORIGIN/../../gopacket_amd:$ORIGIN/../../oracle:/opt/rocm/lib"],
+                       check=True)
+    return ABI_HOST
+
+
 if __name__ == "__main__":
     force = "--force" in sys.argv
     print(build_lib(force=force, verbose=True))
     print(build_oracle(force=force))
+    print(build_abi_host(force=force))

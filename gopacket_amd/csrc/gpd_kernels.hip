@@ -775,29 +775,32 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   return v;
 }
 
-// P[c] = LE-domain sum of the window's 16-byte chunks below c, for c in [0, 512], written
-// to LDS at pfx.  Lane l sums chunks [8l, 8l + 8); bytes past the window's end only reach
-// entries beyond it.
+// P[c] = LE-domain sum of the window's 16-byte chunks below c, for c in [0, STAGE/16],
+// written to LDS at pfx.  Lane l sums chunks [K l, K l + K), K = STAGE/1024; bytes past the
+// window's end only reach entries beyond it.
+template <int STAGE>
 __device__ __forceinline__ void window_prefix(uint32_t buf, uint32_t pfx, uint32_t lane) {
-  uint32_t c[8];
+  constexpr int K = STAGE / 1024;
+  uint32_t c[K];
 #pragma unroll
-  for (int j = 0; j < 8; j++) {
-    const uint4 q = *reinterpret_cast<const uint4 *>(g_lds + buf + 128u * lane + 16u * j);
+  for (int j = 0; j < K; j++) {
+    const uint4 q = *reinterpret_cast<const uint4 *>(g_lds + buf + 16u * K * lane + 16u * j);
     c[j] = dot2(q.w, 0x00010001u, dot2(q.z, 0x00010001u,
                 dot2(q.y, 0x00010001u, dot2(q.x, 0x00010001u, 0u))));
   }
   uint32_t run = 0;
 #pragma unroll
-  for (int j = 0; j < 8; j++) {
+  for (int j = 0; j < K; j++) {
     const uint32_t v = c[j];
     c[j] = run;  // exclusive within the block
     run += v;
   }
   const uint32_t incl = wave_incl_scan(run), base = incl - run;
-  uint4 *d = reinterpret_cast<uint4 *>(g_lds + pfx + 32u * lane);
-  d[0] = uint4{base + c[0], base + c[1], base + c[2], base + c[3]};
-  d[1] = uint4{base + c[4], base + c[5], base + c[6], base + c[7]};
-  if (lane == 63u) *reinterpret_cast<uint32_t *>(g_lds + pfx + 2048u) = incl;
+  uint4 *d = reinterpret_cast<uint4 *>(g_lds + pfx + 4u * K * lane);
+#pragma unroll
+  for (int j = 0; j < K / 4; j++)
+    d[j] = uint4{base + c[4 * j], base + c[4 * j + 1], base + c[4 * j + 2], base + c[4 * j + 3]};
+  if (lane == 63u) *reinterpret_cast<uint32_t *>(g_lds + pfx + 4u * K * 64u) = incl;
 }
 
 // p: LDS address of the packet's first byte; len: its length.  CS / HASH: the fused
@@ -816,7 +819,8 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
   uint64_t codes = 0, nh = 0, th = 0;
   uint32_t nc = 0, trunc = 0, stop = 0;
   uint32_t net = 0, tp = 0, ip4 = 0, ipcs = 0;
-  uint32_t tp_off = 0, tp_len = 0, tp_ps = 0;  // the last transport and its pseudo-header sum
+  uint32_t tp_off = 0, tp_len = 0, tp_pl = 0;  // the last transport; its proto + length terms
+  uint32_t tp_kind = 0, ps4 = 0, ps6 = 0;      // its network object kind; each kind's addresses
   U128 c0{0, 0, 0, 0}, ct{0, 0, 0, 0};        // its segment's first / ragged-last chunk
   uint32_t b = 0, lim = len;                   // this pass's Ethernet offset; end of its data
   auto put = [&](uint32_t code) { codes |= (uint64_t)code << (16 + 4 * nc); nc++; };
@@ -889,6 +893,7 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
         ip4 = 1;
       }
       if (HASH) nh = flow_fast(fnv_start<4>(W[3]), fnv_start<4>(W[4]), 1u);  // ip4.go:63-65
+      ps4 = ps;
       net = 1;
       put(GPD_C_IPV4);
       lim = l3 + 20u + plen;  // Length trims the payload (and Ethernet padding)
@@ -903,6 +908,7 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
         const H64 hd = fnv_more(fnv_more(fnv_more(fnv_start<4>(W[6]), W[7]), W[8]), W[9]);
         nh = flow_fast(hs, hd, 2u);
       }
+      ps6 = ps;
       net = 2;
       put(GPD_C_IPV6);
       lim = l3 + 40u + plen;
@@ -939,8 +945,12 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
     }
     tp = g;
     if (HASH) th = flow_fast(fnv_start<2>(tx), fnv_start<2>(tx >> 16), g == 1u ? 4u : 5u);
-    // pseudo-header protocol and length as LE-domain words (seg < 2^16 in a window)
-    tp_ps = ps + (g == 1u ? 0x0600u : 0x1100u) + __builtin_amdgcn_perm(0u, seg, 0x0C0C0001u);
+    // pseudo-header protocol and length as LE-domain words (seg < 2^16 in a window); the
+    // addresses are added at the end from the network object of this kind as the call
+    // leaves it (SetNetworkLayerForChecksum(&ip4) reads the reused object: for VXLAN whose
+    // inner pass stops before a transport, the inner header's addresses)
+    tp_pl = (g == 1u ? 0x0600u : 0x1100u) + __builtin_amdgcn_perm(0u, seg, 0x0C0C0001u);
+    tp_kind = net;
     tp_off = l4;
     tp_len = seg;
     c0 = n0;
@@ -956,10 +966,11 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
     if (pl4 == 8u) break;
   }
   // ---- outputs, composed exactly as decode_packet does
+  const uint32_t tp_ps = tp_pl + (tp_kind == 1u ? ps4 : ps6);
   uint32_t st = (stop ? F.unsup : GPD_ST_OK) | (trunc << 2) | (nc << 4);
   uint32_t cs = 0;
   if (HASH) {
-    st |= (1u << 16) | (net << 20) | (tp ? (1u << 17) | ((tp == 1 ? 4u : 5u) << 24) : 0u);
+    st |= (net ? (1u << 16) | (net << 20) : 0u) | (tp ? (1u << 17) | ((tp == 1 ? 4u : 5u) << 24) : 0u);
   }
   sg.b = 0;
   if (COOP && CS && tp && tp_len >= 64u && !((p + tp_off) & 1u)) {
@@ -1165,10 +1176,10 @@ __device__ __forceinline__ void wait_window(uint32_t nstores) {
   }
 }
 
-// LDS bytes per wave: two windows, two descriptor slots, and (fast kernel, 8 KiB windows)
-// the 513 chunk prefix sums of the cooperative segment checksum.
+// LDS bytes per wave: two windows, two descriptor slots, and (fast kernel, windows of 8 KiB
+// and more) the stage/16 + 1 chunk prefix sums of the cooperative segment checksum.
 __host__ __device__ constexpr uint32_t wave_lds_bytes(int stage, bool fast) {
-  return 2u * stage + 1024u + ((fast && stage == 8192) ? 2064u : 0u);
+  return 2u * stage + 1024u + ((fast && stage >= 8192) ? (uint32_t)stage / 4u + 16u : 0u);
 }
 
 // WAVES waves per workgroup; each wave owns 64-packet tiles t, t + W, ... (grid stride).  A
@@ -1196,7 +1207,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void decode_kernel(KParams P) {
   __syncthreads();
   const Tab<PAGES> T{P.pages,    P.eth_base, P.tcp_base, P.udp_base, P.eth_bits,
                      P.tcp_bits, P.udp_bits, P.eth_mult, P.tcp_mult, P.udp_mult};
-  constexpr bool COOP = FAST && STAGE == 8192;  // long segments: wave-cooperative checksum
+  constexpr bool COOP = FAST && STAGE >= 8192;  // long segments: wave-cooperative checksum
   const uint32_t img = (P.image_words * 4u + 15u) & ~15u;
   const uint32_t bufs = img + wave * wave_lds_bytes(STAGE, FAST);
   const uint32_t dslots = bufs + 2u * STAGE;  // two slots of 64 offsets + 64 caplens
@@ -1326,7 +1337,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void decode_kernel(KParams P) {
     if constexpr (COOP) {  // long segments of this window: chunk prefix sums, shared
       if (__any(sg.b > sg.a)) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        window_prefix(buf, pfx, lane);
+        window_prefix<STAGE>(buf, pfx, lane);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (sg.b > sg.a) {
           const uint32_t mid = lds_u32(pfx + 4u * sg.b) - lds_u32(pfx + 4u * sg.a);

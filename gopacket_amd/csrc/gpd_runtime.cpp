@@ -312,8 +312,10 @@ int gpd_ctx_create(int device, const gpd_config *cfg, gpd_ctx **out) {
   if (!out) return set_err(GPD_ERR_INVALID, "gpd_ctx_create: out is NULL");
   *out = nullptr;
   int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
-    return set_err(GPD_ERR_NODEVICE, "gpd_ctx_create: no HIP device available");
+  const hipError_t dc = hipGetDeviceCount(&ndev);
+  if (dc != hipSuccess || ndev == 0)
+    return set_err(GPD_ERR_NODEVICE, "gpd_ctx_create: no HIP device available (%s, %d devices)",
+                   hipGetErrorString(dc), ndev);
   if (device < 0 || device >= ndev)
     return set_err(GPD_ERR_INVALID, "gpd_ctx_create: device %d out of range [0,%d)", device, ndev);
   gpd_config defaults{};

@@ -77,3 +77,31 @@ def test_ctx_create_fails_loudly_without_device():
     rc = _lib.lib.gpd_ctx_create(0, None, C.byref(h))
     assert rc != 0 and h.value is None
     assert b"device" in _lib.lib.gpd_last_error_string()
+
+
+@pytest.mark.gpu
+def test_c_host_program_on_the_abi(tmp_path):
+    """tests/c/abi_host: a plain C program (no Python, no torch in its process — the cgo case)
+    decodes through gpd_decode on its own hipMalloc'ed buffers and stream and through
+    gpd_decode_host; both must equal the oracle bit for bit."""
+    import golden_cases as G
+    from gopacket_amd import synth
+    from gopacket_amd.batch import PacketBatch
+    exe = os.path.join(ROOT, "tests", "c", "abi_host")
+    assert os.path.exists(exe), "build tests/c/abi_host first (__graft_entry__.build())"
+    pkts = [G.case_bytes(c) for c in G.load()["cases"]]
+    pkts += [p[:k] for p in pkts[:8] for k in range(0, len(p), 3)]
+    mixed = synth.make_mixed(3000)
+    pkts += [mixed.packet(i) for i in range(mixed.n)]
+    for decoders, options in ((0xFFF, 0), (0x3FF, 1), (0x1 | 0x4 | 0x400 | 0x20 | 0x40 | 0x100, 0)):
+        b = PacketBatch.from_packets(pkts)
+        f = tmp_path / f"batch_{decoders:x}_{options}.bin"
+        with open(f, "wb") as fh:
+            fh.write(np.array([b.data_len, b.n], np.uint64).tobytes())
+            fh.write(np.array([decoders, options], np.uint32).tobytes())
+            fh.write(b.data[:b.data_len].tobytes())
+            fh.write(b.offset.astype(np.uint32).tobytes())
+            fh.write(b.caplen.astype(np.uint32).tobytes())
+        r = subprocess.run([exe, str(f)], capture_output=True, text=True, timeout=90)
+        assert r.returncode == 0, r.stdout + r.stderr
+        assert r.stdout.strip() == f"abi_host ok {b.n}"
