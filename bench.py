@@ -148,6 +148,39 @@ def summarize(workload, n, world, steps, warmup, elapsed, kern_ms, kern_ms_max, 
     }
 
 
+def bench_flows(parser, dev_batch, n, args, stream, local):
+    """F3 diagnostic: decode (with header offsets) then find-or-create every packet's flow
+    record in an empty table (gpd_flow_insert: insert + key-verify launches), timed with HIP
+    events on the launch stream around the insert alone."""
+    import torch
+    from gopacket_amd import flows as FL
+    from gopacket_amd import parser as P
+    res = P.DeviceResult(n, local, ext=False, hdr_off=True)
+    parser.decode_device(dev_batch, res, stream)
+    cap = 1 << max(10, (2 * n - 1).bit_length())  # load factor <= 1/2
+    ft = FL.NewFlowTable(parser, cap)
+    fid = torch.empty(n, dtype=torch.int32, device=f"cuda:{local}")
+    steps = max(3, min(args.steps, 10))
+    ins, rst = [], []
+    for k in range(steps + 1):
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        e[0].record(stream)
+        ft.Reset(stream)
+        e[1].record(stream)
+        ft.Insert(dev_batch, res, fid, 0, stream)
+        e[2].record(stream)
+        torch.cuda.synchronize(local)
+        if k:  # the first round is warm-up
+            rst.append(e[0].elapsed_time(e[1]))
+            ins.append(e[1].elapsed_time(e[2]))
+    st = ft.Stats(stream)
+    ms = float(np.mean(ins))
+    return {"diag": "F3 flow table (not the metric)", "packets": n, "insert_ms": round(ms, 4),
+            "insert_Mpackets_per_s": round(n / ms / 1e3, 1), "reset_ms": round(float(np.mean(rst)), 4),
+            "capacity": st["capacity"], "flows": st["flows"], "keyed_packets": st["packets"],
+            "collisions": st["collisions"], "full": st["full"]}
+
+
 def replay_pcap(parser, cap, n, total, threads):
     """PCIe-inclusive rate: the capture in (registered) host memory replayed through
     gpd_decode_pcap — native index, raw capture bytes H2D, decode, results D2H — until `total`
@@ -188,6 +221,9 @@ def main():
     ap.add_argument("--replay", type=int, default=0, help="pcap64: also replay the capture from "
                     "host memory through gpd_decode_pcap until this many packets were decoded "
                     "(PCIe-inclusive rate; a diagnostic beside the device-resident value)")
+    ap.add_argument("--flows", action="store_true",
+                    help="diagnostic: also time the F3 flow table (gpd_flow_insert) on the decoded "
+                    "batch; printed as a separate line, never the reported metric")
     ap.add_argument("--ablate", default="", help="diagnostics only: 'nocsum', 'nohash' or both "
                     "(comma separated); never used for the reported metric")
     args = ap.parse_args()
@@ -223,7 +259,7 @@ def main():
                      "index_Mrec_per_s": round(n / t_index / 1e6, 1),
                      "index_threads": NP.last_walk_stats()[0]}
     dev_batch = P.DeviceBatch(batch, local)
-    dev_res = P.DeviceResult(n, local, ext=False)
+    dev_res = P.DeviceResult(n, local, ext=False, hdr_off=False)  # the 32-B record
     parser = P.NewDecodingLayerParser(L.LayerTypeEthernet, P.Ethernet(), P.Dot1Q(), P.IPv4(),
                                       P.IPv6(), P.IPv6ExtensionSkipper(), P.TCP(), P.UDP(),
                                       P.VXLAN(), P.Payload(), P.Fragment(), device=local)
@@ -319,6 +355,8 @@ def main():
         out["cpu_baseline"] = cpu_baseline(batch, args.cpu_budget)
     if rank == 0:
         print(json.dumps(out), flush=True)
+    if args.flows and rank == 0:
+        print(json.dumps(bench_flows(parser, dev_batch, n, args, stream, local)), flush=True)
     if dist:
         dist.destroy_process_group()
 

@@ -193,12 +193,14 @@ type Result struct {
 	NetHash  []uint64
 	TpHash   []uint64
 	Checksum []uint32
+	HdrOff   []uint32 // gpd.h header offsets word: where the flows' layers sit
 }
 
 // DecodeBatch decodes every packet of b (host memory, pinned H2D -> kernel -> D2H).
 func (p *BatchDecodingLayerParser) DecodeBatch(b *PacketBatch) (*Result, error) {
 	n := len(b.Offset)
-	r := &Result{make([]uint32, n), make([]uint64, n), make([]uint64, n), make([]uint64, n), make([]uint32, n)}
+	r := &Result{make([]uint32, n), make([]uint64, n), make([]uint64, n), make([]uint64, n), make([]uint32, n),
+		make([]uint32, n)}
 	if n == 0 {
 		return r, nil
 	}
@@ -220,6 +222,7 @@ func (p *BatchDecodingLayerParser) DecodeBatch(b *PacketBatch) (*Result, error) 
 		net_hash: (*C.uint64_t)(unsafe.Pointer(&r.NetHash[0])),
 		tp_hash:  (*C.uint64_t)(unsafe.Pointer(&r.TpHash[0])),
 		csum:     (*C.uint32_t)(unsafe.Pointer(&r.Checksum[0])),
+		hdr_off:  (*C.uint32_t)(unsafe.Pointer(&r.HdrOff[0])),
 	}
 	if err := p.configure(); err != nil {
 		return nil, err
@@ -282,6 +285,48 @@ func (r *Result) Err(i int) error {
 		return errors.New(errorText[(r.Status[i]>>9)&63])
 	}
 	return nil
+}
+
+// lastCode is the position-independent kind of the last decoded layer with one of the two
+// codes (the core record holds the first 12 layers).
+func (r *Result) lastCode(i int, a, b uint64) uint64 {
+	n := int(r.Status[i]>>4) & 31
+	var last uint64
+	for k := 0; k < n && k < C.GPD_CORE_MAX_LAYERS; k++ {
+		if c := (r.Layers[i] >> (16 + 4*uint(k))) & 15; c == a || c == b {
+			last = c
+		}
+	}
+	return last
+}
+
+// NetworkFlow is ip4/ip6.NetworkFlow() after DecodeLayers on packet i (ip4.go:63-65,
+// ip6.go:49-51): the endpoints are slices of the packet bytes at the offset the kernel
+// reported, as the reference's layer structs slice them.
+func (r *Result) NetworkFlow(b *PacketBatch, i int) (gopacket.Flow, bool) {
+	off := r.HdrOff[i] & 0xFFFF
+	pkt := b.Data[b.Offset[i] : b.Offset[i]+b.CapLen[i]]
+	switch r.lastCode(i, C.GPD_C_IPV4, C.GPD_C_IPV6) {
+	case C.GPD_C_IPV4:
+		return gopacket.NewFlow(layers.EndpointIPv4, pkt[off+12:off+16], pkt[off+16:off+20]), true
+	case C.GPD_C_IPV6:
+		return gopacket.NewFlow(layers.EndpointIPv6, pkt[off+8:off+24], pkt[off+24:off+40]), true
+	}
+	return gopacket.Flow{}, false
+}
+
+// TransportFlow is tcp/udp.TransportFlow() after DecodeLayers on packet i (tcp.go:331-333,
+// udp.go:123-125).  Together with NetworkFlow it is the [2]Flow key tcpassembly uses.
+func (r *Result) TransportFlow(b *PacketBatch, i int) (gopacket.Flow, bool) {
+	off := r.HdrOff[i] >> 16
+	pkt := b.Data[b.Offset[i] : b.Offset[i]+b.CapLen[i]]
+	switch r.lastCode(i, C.GPD_C_TCP, C.GPD_C_UDP) {
+	case C.GPD_C_TCP:
+		return gopacket.NewFlow(layers.EndpointTCPPort, pkt[off:off+2], pkt[off+2:off+4]), true
+	case C.GPD_C_UDP:
+		return gopacket.NewFlow(layers.EndpointUDPPort, pkt[off:off+2], pkt[off+2:off+4]), true
+	}
+	return gopacket.Flow{}, false
 }
 
 // NetworkFlowHash is ip4/ip6.NetworkFlow().FastHash() of the last network layer.

@@ -11,7 +11,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GPD_LIB_PATH") or os.path.join(_HERE, "libgpd.so")  # override: A/B only
 
-GPD_ABI_VERSION = 2
+GPD_ABI_VERSION = 3
 GPD_OK = 0
 
 
@@ -28,7 +28,8 @@ class GpdBatch(C.Structure):
 
 class GpdResult(C.Structure):
     _fields_ = [("status", C.c_void_p), ("layers", C.c_void_p), ("net_hash", C.c_void_p),
-                ("tp_hash", C.c_void_p), ("csum", C.c_void_p), ("ext", C.c_void_p)]
+                ("tp_hash", C.c_void_p), ("csum", C.c_void_p), ("ext", C.c_void_p),
+                ("hdr_off", C.c_void_p)]
 
 
 class GpdPcapInfo(C.Structure):
@@ -62,6 +63,15 @@ EXPORTS = {
     "gpd_pcap_last_stats": (None, [C.POINTER(C.c_int)] * 3),
     "gpd_host_register": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
     "gpd_host_unregister": (C.c_int, [C.c_void_p, C.c_void_p]),
+    # include/gpd_flow.h
+    "gpd_flow_create": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.c_void_p)]),
+    "gpd_flow_reset": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "gpd_flow_insert": (C.c_int, [C.c_void_p, C.POINTER(GpdBatch), C.POINTER(GpdResult), C.c_void_p,
+                                  C.c_uint64, C.c_void_p]),
+    "gpd_flow_stats_get": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "gpd_flow_export": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
+                                  C.POINTER(C.c_uint64), C.c_void_p]),
+    "gpd_flow_destroy": (C.c_int, [C.c_void_p]),
 }
 
 GPD_ERR_PCAP = -5

@@ -1,0 +1,347 @@
+// gpd_flow.hip — MI355X flow table (include/gpd_flow.h): find-or-create the connection
+// record of every decoded packet, keyed by its [2]Flow{NetworkFlow(), TransportFlow()}.
+//
+// Reference (paths relative to google/gopacket):
+//   key ............... tcpassembly/assembly.go:289,543 (key{netFlow, t.TransportFlow()}),
+//                       reassembly/tcpassembly.go:389,644
+//   Flow equality ..... flows.go:140-146 (struct fields; NewFlow zero-pads to 16, :214-224)
+//   find-or-create .... tcpassembly/assembly.go:495-511 (StreamPool.getConnection)
+//   endpoints ......... layers/ip4.go:63-65, layers/ip6.go:49-51, layers/tcp.go:331-333,
+//                       layers/udp.go:123-125, layers/endpoints.go:20-32
+//
+// One lane per packet.  The decoder already left, per packet, the EndpointTypes of both
+// flows (status bits 20-27) and where their layers sit (hdr_off), so the key is gathered
+// straight from the packet bytes in HBM: 16+16 address bytes, 4 port bytes, the types.
+// Records live in an open-addressing table of 2^k 80-byte records.  A record is claimed by
+// one 64-bit compare-and-swap of the key's fingerprint; the claimer then stores the key.
+// The per-flow counters are device atomics.  A second launch compares every packet's key
+// with its record's stored key (visible after the launch boundary), so a fingerprint
+// collision is caught and reported instead of silently merging two flows.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "gpd_internal.h"
+#include "../../include/gpd_flow.h"
+
+namespace gpd {
+
+constexpr int kFlowThreads = 256;
+static_assert(sizeof(gpd_flow_rec) == 80, "gpd_flow_rec layout (include/gpd_flow.h)");
+
+enum : uint32_t { FS_FLOWS = 0, FS_PACKETS, FS_NOKEY, FS_FULL, FS_COLL, FS_EXPORT, FS_WORDS = 8 };
+
+struct FlowParams {
+  const uint8_t *data;
+  uint64_t data_len;
+  const uint32_t *offset, *caplen, *status, *hdr_off;
+  uint32_t *flow_id;
+  uint64_t n, base;
+  gpd_flow_rec *tab;
+  uint64_t mask;  // capacity - 1
+  unsigned long long *stats;
+};
+
+// The key of packet i as 10 words: src[16], dst[16], ports (raw wire bytes), types.  Returns
+// false when the packet has no network + transport pair (gpd.h status / hdr_off words).
+__device__ __forceinline__ bool flow_key(const FlowParams &P, uint64_t i, uint32_t (&k)[10]) {
+  const uint32_t st = P.status[i], ho = P.hdr_off[i];
+  const uint32_t nt = (st >> 20) & 15u, tt = (st >> 24) & 15u;
+  const uint32_t no = ho & 0xFFFFu, to = ho >> 16;
+  if (nt == 0 || tt == 0 || no == 0xFFFFu || to == 0xFFFFu) return false;
+  const uint64_t off = min((uint64_t)P.offset[i], P.data_len);
+  const uint8_t *pkt = P.data + off;
+  const uint32_t alen = nt == 1u ? 4u : 16u;
+  const uint8_t *src = pkt + no + (nt == 1u ? 12u : 8u);  // ip4.go:63-65 / ip6.go:49-51
+  const uint8_t *dst = src + alen;
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    uint32_t a = 0, b = 0;
+    if ((uint32_t)w * 4u < alen) {
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        a |= (uint32_t)src[4 * w + j] << (8 * j);
+        b |= (uint32_t)dst[4 * w + j] << (8 * j);
+      }
+    }
+    k[w] = a;  // NewFlow zero-pads the unused address bytes (flows.go:214-224)
+    k[4 + w] = b;
+  }
+  const uint8_t *tp = pkt + to;  // tcp.go:331-333 / udp.go:123-125: ports as raw bytes
+  k[8] = (uint32_t)tp[0] | ((uint32_t)tp[1] << 8) | ((uint32_t)tp[2] << 16) | ((uint32_t)tp[3] << 24);
+  k[9] = nt | (tt << 8) | (alen << 16);
+  return true;
+}
+
+__device__ __forceinline__ uint64_t fingerprint(const uint32_t (&k)[10]) {
+  uint64_t h = 0x9E3779B97F4A7C15ull;
+#pragma unroll
+  for (int w = 0; w < 10; w += 2) {
+    h ^= ((uint64_t)k[w + 1] << 32) | k[w];
+    h *= 0xFF51AFD7ED558CCDull;
+    h ^= h >> 32;
+  }
+  h ^= h >> 33;
+  h *= 0xC4CEB9FE1A85EC53ull;
+  h ^= h >> 33;
+  return h ? h : 1ull;
+}
+
+__device__ __forceinline__ void wave_count(unsigned long long *ctr, bool pred) {
+  const uint64_t m = __ballot(pred);
+  if (m && (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(m))
+    atomicAdd(ctr, (unsigned long long)__popcll(m));
+}
+
+__global__ __launch_bounds__(kFlowThreads) void flow_insert_kernel(FlowParams P) {
+  for (uint64_t i = blockIdx.x * (uint64_t)kFlowThreads + threadIdx.x; i - threadIdx.x < P.n;
+       i += (uint64_t)gridDim.x * kFlowThreads) {
+    const bool live = i < P.n;
+    uint32_t k[10];
+    const bool keyed = live && flow_key(P, i, k);
+    bool created = false, full = false;
+    uint64_t s = 0;
+    if (keyed) {
+      const uint64_t fp = fingerprint(k);
+      s = fp & P.mask;
+      uint64_t probe = 0;
+      for (; probe <= P.mask; probe++) {  // every lane leaves after at most capacity probes
+        const unsigned long long old =
+            atomicCAS(reinterpret_cast<unsigned long long *>(&P.tab[s].fp), 0ull, (unsigned long long)fp);
+        if (old == 0ull) {  // claimed: store the key (read by the verify launch)
+          gpd_flow_rec &r = P.tab[s];
+          uint32_t *w = reinterpret_cast<uint32_t *>(r.src);
+#pragma unroll
+          for (int j = 0; j < 9; j++) w[j] = k[j];  // src, dst, ports
+          r.net_type = (uint8_t)(k[9] & 0xFFu);
+          r.tp_type = (uint8_t)((k[9] >> 8) & 0xFFu);
+          r.addr_len = (uint8_t)(k[9] >> 16);
+          created = true;
+          break;
+        }
+        if (old == fp) break;
+        s = (s + 1) & P.mask;
+      }
+      if (probe > P.mask) full = true;
+    }
+    const bool counted = keyed && !full;
+    if (counted) {
+      const uint64_t seq = P.base + i;
+      gpd_flow_rec &r = P.tab[s];
+      atomicMin(reinterpret_cast<unsigned long long *>(&r.first), (unsigned long long)seq);
+      atomicMax(reinterpret_cast<unsigned long long *>(&r.last), (unsigned long long)seq);
+      atomicAdd(reinterpret_cast<unsigned long long *>(&r.packets), 1ull);
+      atomicAdd(reinterpret_cast<unsigned long long *>(&r.bytes), (unsigned long long)P.caplen[i]);
+    }
+    if (live) P.flow_id[i] = !keyed ? GPD_FLOW_NONE : full ? GPD_FLOW_FULL : (uint32_t)s;
+    wave_count(P.stats + FS_FLOWS, created);
+    wave_count(P.stats + FS_PACKETS, counted);
+    wave_count(P.stats + FS_NOKEY, live && !keyed);
+    wave_count(P.stats + FS_FULL, full);
+  }
+}
+
+// Second pass: every packet's key against its record's stored key.
+__global__ __launch_bounds__(kFlowThreads) void flow_verify_kernel(FlowParams P) {
+  for (uint64_t i = blockIdx.x * (uint64_t)kFlowThreads + threadIdx.x; i - threadIdx.x < P.n;
+       i += (uint64_t)gridDim.x * kFlowThreads) {
+    bool bad = false;
+    if (i < P.n) {
+      const uint32_t id = P.flow_id[i];
+      uint32_t k[10];
+      if (id < GPD_FLOW_FULL && flow_key(P, i, k)) {
+        const gpd_flow_rec &r = P.tab[id];
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(r.src);
+        bool same = k[9] == ((uint32_t)r.net_type | ((uint32_t)r.tp_type << 8) | ((uint32_t)r.addr_len << 16));
+#pragma unroll
+        for (int j = 0; j < 9; j++) same = same && w[j] == k[j];
+        if (!same) {
+          P.flow_id[i] = id | GPD_FLOW_COLLISION;
+          bad = true;
+        }
+      }
+    }
+    wave_count(P.stats + FS_COLL, bad);
+  }
+}
+
+__global__ __launch_bounds__(kFlowThreads) void flow_reset_kernel(gpd_flow_rec *tab, uint64_t cap) {
+  for (uint64_t s = blockIdx.x * (uint64_t)kFlowThreads + threadIdx.x; s < cap;
+       s += (uint64_t)gridDim.x * kFlowThreads) {
+    gpd_flow_rec r{};
+    r.first = ~0ull;
+    tab[s] = r;
+  }
+}
+
+__global__ __launch_bounds__(kFlowThreads) void flow_export_kernel(const gpd_flow_rec *tab, uint64_t cap,
+                                                                  gpd_flow_rec *out, uint32_t *idx,
+                                                                  uint64_t max,
+                                                                  unsigned long long *stats) {
+  for (uint64_t s = blockIdx.x * (uint64_t)kFlowThreads + threadIdx.x; s < cap;
+       s += (uint64_t)gridDim.x * kFlowThreads) {
+    if (tab[s].fp != 0) {
+      const unsigned long long j = atomicAdd(stats + FS_EXPORT, 1ull);
+      if (j < max) {
+        out[j] = tab[s];
+        idx[j] = (uint32_t)s;
+      }
+    }
+  }
+}
+
+}  // namespace gpd
+
+struct gpd_flowtable {
+  int device = 0;
+  int num_cus = 256;
+  gpd_flow_rec *tab = nullptr;
+  uint64_t cap = 0;
+  unsigned long long *stats = nullptr;  // FS_WORDS counters
+};
+
+#define FLOW_TRY(expr)                                                                      \
+  do {                                                                                     \
+    hipError_t e_ = (expr);                                                                \
+    if (e_ != hipSuccess)                                                                  \
+      return gpd::set_error(GPD_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_));          \
+  } while (0)
+
+static unsigned grid_for(uint64_t work, int num_cus) {
+  const uint64_t blocks = (work + gpd::kFlowThreads - 1) / gpd::kFlowThreads;
+  return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)num_cus * 8));
+}
+
+extern "C" {
+
+int gpd_flow_create(gpd_ctx *ctx, uint64_t capacity, gpd_flowtable **out) {
+  if (!ctx || !out) return gpd::set_error(GPD_ERR_INVALID, "gpd_flow_create: null argument");
+  *out = nullptr;
+  if (capacity == 0 || capacity > (1ull << 31))
+    return gpd::set_error(GPD_ERR_INVALID, "gpd_flow_create: capacity %llu outside [1, 2^31]",
+                          (unsigned long long)capacity);
+  uint64_t cap = 1;
+  while (cap < capacity) cap <<= 1;
+  gpd_flowtable *ft = new gpd_flowtable;
+  ft->device = gpd::ctx_device(ctx);
+  ft->num_cus = gpd::ctx_num_cus(ctx);
+  ft->cap = cap;
+  hipError_t e = hipSetDevice(ft->device);
+  if (e == hipSuccess) e = hipMalloc(&ft->tab, cap * sizeof(gpd_flow_rec));
+  if (e == hipSuccess) e = hipMalloc(&ft->stats, gpd::FS_WORDS * sizeof(unsigned long long));
+  if (e != hipSuccess) {
+    gpd_flow_destroy(ft);
+    return gpd::set_error(e == hipErrorOutOfMemory ? GPD_ERR_NOMEM : GPD_ERR_HIP,
+                          "gpd_flow_create: %s", hipGetErrorString(e));
+  }
+  int rc = gpd_flow_reset(ft, nullptr);
+  if (rc == GPD_OK) rc = hipDeviceSynchronize() == hipSuccess ? GPD_OK : GPD_ERR_HIP;
+  if (rc != GPD_OK) {
+    gpd_flow_destroy(ft);
+    return rc;
+  }
+  *out = ft;
+  return GPD_OK;
+}
+
+int gpd_flow_reset(gpd_flowtable *ft, void *stream) {
+  if (!ft) return gpd::set_error(GPD_ERR_INVALID, "gpd_flow_reset: null table");
+  FLOW_TRY(hipSetDevice(ft->device));
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(gpd::flow_reset_kernel, dim3(grid_for(ft->cap, ft->num_cus)),
+                     dim3(gpd::kFlowThreads), 0, s, ft->tab, ft->cap);
+  FLOW_TRY(hipGetLastError());
+  FLOW_TRY(hipMemsetAsync(ft->stats, 0, gpd::FS_WORDS * sizeof(unsigned long long), s));
+  return GPD_OK;
+}
+
+int gpd_flow_insert(gpd_flowtable *ft, const gpd_batch *in, const gpd_result *res,
+                    uint32_t *flow_id, uint64_t index_base, void *stream) {
+  if (!ft || !in || !res || !flow_id)
+    return gpd::set_error(GPD_ERR_INVALID, "gpd_flow_insert: null argument");
+  if (!res->status || !res->hdr_off)
+    return gpd::set_error(GPD_ERR_INVALID, "gpd_flow_insert: the results need status and hdr_off");
+  if (in->n == 0) return GPD_OK;
+  if (!in->data || !in->offset || !in->caplen)
+    return gpd::set_error(GPD_ERR_INVALID, "gpd_flow_insert: null batch array");
+  FLOW_TRY(hipSetDevice(ft->device));
+  gpd::FlowParams P{in->data, in->data_len, in->offset, in->caplen, res->status, res->hdr_off,
+                    flow_id, in->n, index_base, ft->tab, ft->cap - 1, ft->stats};
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid(grid_for(in->n, ft->num_cus)), block(gpd::kFlowThreads);
+  hipLaunchKernelGGL(gpd::flow_insert_kernel, grid, block, 0, s, P);
+  FLOW_TRY(hipGetLastError());
+  hipLaunchKernelGGL(gpd::flow_verify_kernel, grid, block, 0, s, P);
+  FLOW_TRY(hipGetLastError());
+  return GPD_OK;
+}
+
+int gpd_flow_stats_get(gpd_flowtable *ft, gpd_flow_stats *out, void *stream) {
+  if (!ft || !out) return gpd::set_error(GPD_ERR_INVALID, "gpd_flow_stats_get: null argument");
+  FLOW_TRY(hipSetDevice(ft->device));
+  unsigned long long h[gpd::FS_WORDS];
+  FLOW_TRY(hipMemcpyAsync(h, ft->stats, sizeof h, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  FLOW_TRY(hipStreamSynchronize((hipStream_t)stream));
+  out->flows = h[gpd::FS_FLOWS];
+  out->packets = h[gpd::FS_PACKETS];
+  out->no_key = h[gpd::FS_NOKEY];
+  out->full = h[gpd::FS_FULL];
+  out->collisions = h[gpd::FS_COLL];
+  out->capacity = ft->cap;
+  return GPD_OK;
+}
+
+int gpd_flow_export(gpd_flowtable *ft, gpd_flow_rec *out, uint32_t *rec_index, uint64_t max,
+                    uint64_t *n, void *stream) {
+  if (!ft || !out || !n) return gpd::set_error(GPD_ERR_INVALID, "gpd_flow_export: null argument");
+  *n = 0;
+  FLOW_TRY(hipSetDevice(ft->device));
+  hipStream_t s = (hipStream_t)stream;
+  gpd_flow_stats st;
+  int rc = gpd_flow_stats_get(ft, &st, stream);
+  if (rc) return rc;
+  const uint64_t m = std::min<uint64_t>(max, st.flows);
+  if (m == 0) return GPD_OK;
+  gpd_flow_rec *d_out = nullptr;
+  uint32_t *d_idx = nullptr;
+  FLOW_TRY(hipMalloc(&d_out, m * sizeof(gpd_flow_rec)));
+  hipError_t e = hipMalloc(&d_idx, m * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMemsetAsync(ft->stats + gpd::FS_EXPORT, 0, sizeof(unsigned long long), s);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(gpd::flow_export_kernel, dim3(grid_for(ft->cap, ft->num_cus)),
+                       dim3(gpd::kFlowThreads), 0, s, ft->tab, ft->cap, d_out, d_idx, m, ft->stats);
+    e = hipGetLastError();
+  }
+  std::vector<gpd_flow_rec> recs(m);
+  std::vector<uint32_t> idx(m);
+  if (e == hipSuccess) e = hipMemcpyAsync(recs.data(), d_out, m * sizeof(gpd_flow_rec), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(idx.data(), d_idx, m * sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  (void)hipFree(d_out);
+  (void)hipFree(d_idx);
+  if (e != hipSuccess) return gpd::set_error(GPD_ERR_HIP, "gpd_flow_export: %s", hipGetErrorString(e));
+  std::vector<uint64_t> order(m);
+  for (uint64_t j = 0; j < m; j++) order[j] = j;
+  std::sort(order.begin(), order.end(), [&](uint64_t a, uint64_t b) {
+    return recs[a].first != recs[b].first ? recs[a].first < recs[b].first : idx[a] < idx[b];
+  });
+  for (uint64_t j = 0; j < m; j++) {
+    out[j] = recs[order[j]];
+    if (rec_index) rec_index[j] = idx[order[j]];
+  }
+  *n = m;
+  return GPD_OK;
+}
+
+int gpd_flow_destroy(gpd_flowtable *ft) {
+  if (!ft) return GPD_OK;
+  (void)hipSetDevice(ft->device);
+  if (ft->tab) (void)hipFree(ft->tab);
+  if (ft->stats) (void)hipFree(ft->stats);
+  delete ft;
+  return GPD_OK;
+}
+
+}  // extern "C"

@@ -57,6 +57,7 @@ struct KParams {
   uint64_t *tp_hash;
   uint32_t *csum;
   gpd_ext_rec *ext;
+  uint32_t *hdr_off;
   const uint32_t *image;       // LUT + ipproto (+ hash tables in HASH mode); staged into LDS
   const uint16_t *pages;       // PAGES mode: two-level page tables in global memory
   uint32_t image_words;
@@ -87,6 +88,10 @@ hipError_t launch_decode(const KParams &P, hipStream_t stream, int num_cus);
 
 // Host side: set the thread's gpd_last_error_string() text and return `code` (gpd_runtime.cpp).
 int set_error(int code, const char *fmt, ...);
+
+// Host side: the device and compute-unit count of a context (gpd_runtime.cpp).
+int ctx_device(const gpd_ctx *ctx);
+int ctx_num_cus(const gpd_ctx *ctx);
 
 // Host side: the sequential pcap record walk over buf[pos:len), built in parallel
 // (gpd_pcap.cpp; semantics in include/gpd_pcap.h).  Positions are record-header offsets.

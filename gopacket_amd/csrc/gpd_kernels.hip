@@ -248,7 +248,12 @@ struct Out {
   uint64_t layers;
   uint64_t net_hash, tp_hash;
   uint32_t csum;
+  uint32_t hoff;  // gpd.h header offsets word
 };
+
+__device__ __forceinline__ uint32_t hdr_word(bool net, uint32_t net_off, bool tp, uint32_t tp_off) {
+  return (net ? min(net_off, 0xFFFFu) : 0xFFFFu) | ((tp ? min(tp_off, 0xFFFFu) : 0xFFFFu) << 16);
+}
 
 #define GPD_FAIL(code, x0, x1) \
   do { err = (code); a0 = (x0); a1 = (x1); goto fail; } while (0)
@@ -518,12 +523,13 @@ done:
 
   uint64_t nhash = 0, thash = 0;
   uint32_t cs = 0;
+  st |= (last_net << 20) | (last_tp ? (last_tp == 1 ? 4u : 5u) << 24 : 0u);  // endpoint types
   uint32_t v4[2] = {0, 0};  // ip4 src/dst words, shared by the net hash and the pseudo-header
   if (last_net == 1 || (last_tp && tp_net == 1)) load_words(s, ip4_off + 12, v4);
   if (!(options & GPD_OPT_NO_FLOW_HASH)) {
     if (last_net == 1) {  // ip4.NetworkFlow(), ip4.go:63-65
       nhash = flow_mix(fnv_word(kFnvBasis, v4[0], 4), fnv_word(kFnvBasis, v4[1], 4), 1u);
-      st |= (1u << 16) | (1u << 20);
+      st |= 1u << 16;
     } else if (last_net == 2) {  // ip6.NetworkFlow(), ip6.go:49-51
       uint32_t w[8];
       load_words(s, ip6_off + 8, w);
@@ -531,14 +537,14 @@ done:
 #pragma unroll
       for (int k = 0; k < 4; k++) { hs = fnv_word(hs, w[k], 4); hd = fnv_word(hd, w[k + 4], 4); }
       nhash = flow_mix(hs, hd, 2);
-      st |= (1u << 16) | (2u << 20);
+      st |= 1u << 16;
     }
     if (last_tp) {  // tcp/udp.TransportFlow(), tcp.go:331-333, udp.go:123-125
       uint32_t w[1];
       load_words(s, last_tp == 1 ? tcp_off : udp_off, w);
       uint32_t ept = last_tp == 1 ? 4u : 5u;
       thash = flow_mix(fnv_word(kFnvBasis, w[0], 2), fnv_word(kFnvBasis, w[0] >> 16, 2), ept);
-      st |= (1u << 17) | (ept << 24);
+      st |= 1u << 17;
     }
   }
   if (!(options & GPD_OPT_NO_CHECKSUMS)) {
@@ -582,6 +588,8 @@ done:
   o.net_hash = nhash;
   o.tp_hash = thash;
   o.csum = cs;
+  o.hoff = hdr_word(last_net != 0, last_net == 1 ? ip4_off : ip6_off, last_tp != 0,
+                    last_tp == 1 ? tcp_off : udp_off);
   if (EXT) {
     gpd_ext_rec e;
     e.layer_codes[0] = ecodes0;
@@ -821,6 +829,7 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
   uint32_t net = 0, tp = 0, ip4 = 0, ipcs = 0;
   uint32_t tp_off = 0, tp_len = 0, tp_pl = 0;  // the last transport; its proto + length terms
   uint32_t tp_kind = 0, ps4 = 0, ps6 = 0;      // its network object kind; each kind's addresses
+  uint32_t net_off = 0;                        // the last network header
   U128 c0{0, 0, 0, 0}, ct{0, 0, 0, 0};        // its segment's first / ragged-last chunk
   uint32_t b = 0, lim = len;                   // this pass's Ethernet offset; end of its data
   auto put = [&](uint32_t code) { codes |= (uint64_t)code << (16 + 4 * nc); nc++; };
@@ -895,6 +904,7 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
       if (HASH) nh = flow_fast(fnv_start<4>(W[3]), fnv_start<4>(W[4]), 1u);  // ip4.go:63-65
       ps4 = ps;
       net = 1;
+      net_off = l3;
       put(GPD_C_IPV4);
       lim = l3 + 20u + plen;  // Length trims the payload (and Ethernet padding)
     } else if (dec == D_IP6) {  // ip6.go:221-278 without hop-by-hop
@@ -910,6 +920,7 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
       }
       ps6 = ps;
       net = 2;
+      net_off = l3;
       put(GPD_C_IPV6);
       lim = l3 + 40u + plen;
     } else {
@@ -969,9 +980,8 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
   const uint32_t tp_ps = tp_pl + (tp_kind == 1u ? ps4 : ps6);
   uint32_t st = (stop ? F.unsup : GPD_ST_OK) | (trunc << 2) | (nc << 4);
   uint32_t cs = 0;
-  if (HASH) {
-    st |= (net ? (1u << 16) | (net << 20) : 0u) | (tp ? (1u << 17) | ((tp == 1 ? 4u : 5u) << 24) : 0u);
-  }
+  st |= (net << 20) | (tp ? (tp == 1 ? 4u : 5u) << 24 : 0u);  // endpoint types (gpd.h)
+  if (HASH) st |= (net ? 1u << 16 : 0u) | (tp ? 1u << 17 : 0u);
   sg.b = 0;
   if (COOP && CS && tp && tp_len >= 64u && !((p + tp_off) & 1u)) {
     // head [S, A) and tail [B, E) from their aligned chunks; [A, B) from the prefix sums
@@ -1005,6 +1015,7 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
     o.net_hash = HASH ? nh : 0;
     o.tp_hash = HASH ? th : 0;
     o.csum = ip4 ? ipcs : 0u;  // the transport half is added by the caller
+    o.hoff = hdr_word(net != 0, net_off, tp != 0, tp_off);
     return true;
   }
   if (CS) {
@@ -1041,6 +1052,7 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
   o.net_hash = HASH ? nh : 0;
   o.tp_hash = HASH ? th : 0;
   o.csum = cs;
+  o.hoff = hdr_word(net != 0, net_off, tp != 0, tp_off);
   return true;
 }
 
@@ -1058,6 +1070,7 @@ __device__ __forceinline__ void store_out(const KParams &P, uint32_t i, const Ou
     if (P.net_hash) __builtin_nontemporal_store(o.net_hash, P.net_hash + i);
     if (P.tp_hash) __builtin_nontemporal_store(o.tp_hash, P.tp_hash + i);
     if (P.csum) __builtin_nontemporal_store(o.csum, P.csum + i);
+    if (P.hdr_off) __builtin_nontemporal_store(o.hoff, P.hdr_off + i);
     return;
   }
   P.status[i] = o.status;
@@ -1065,6 +1078,7 @@ __device__ __forceinline__ void store_out(const KParams &P, uint32_t i, const Ou
   if (P.net_hash) P.net_hash[i] = o.net_hash;
   if (P.tp_hash) P.tp_hash[i] = o.tp_hash;
   if (P.csum) P.csum[i] = o.csum;
+  if (P.hdr_off) P.hdr_off[i] = o.hoff;
 }
 
 // A window of the batch buffer: bytes [base, base + nbytes) (base 16-aligned).
@@ -1266,7 +1280,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void decode_kernel(KParams P) {
   uint32_t valid_d = valid_p, big_d = big0;
   bool first_d = true;
   uint32_t cur = 0;  // buffer of the window to decode
-  Out res{0, 0, 0, 0, 0};
+  Out res{0, 0, 0, 0, 0, 0};
   uint32_t fb = 0;
   PH_DECL
   for (;;) {
@@ -1322,7 +1336,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void decode_kernel(KParams P) {
     const uint32_t buf = bufs + cur * STAGE;
     Seg sg{0, 0, 0};
     if (cov_d && (P.options & kDiagSkipDecode)) {  // diagnostics: data movement only
-      res = Out{g_lds[buf + ((off_d - Wd.base) & ~15u)], 0, 0, 0, 0};
+      res = Out{g_lds[buf + ((off_d - Wd.base) & ~15u)], 0, 0, 0, 0, 0};
     } else if (cov_d) {
       const LdsSrc<SWZ> src{buf, off_d - Wd.base};
       if constexpr (FAST) {
@@ -1436,14 +1450,12 @@ static int geom() {
 // the fast kernel reads headers at any byte address: linear windows
 template <bool CS, bool HASH>
 static hipError_t launch_fast(const KParams &P, hipStream_t stream, int num_cus) {
-  if (geom() == 2) {  // A/B: register budget for 4 waves per SIMD
-    if (P.stage == 4096)
-      return launch_t<4096, true, false, false, false, 4, CS, HASH, 4>(P, stream, num_cus);
-    return launch_t<8192, true, false, false, false, 4, CS, HASH, 4>(P, stream, num_cus);
-  }
+  // Register budgets match what LDS admits: 4 KiB windows fit four 4-wave workgroups per CU
+  // (4 waves per SIMD, <= 128 VGPRs each), 8 KiB windows two (2 waves per SIMD).  Without
+  // the bound the compiler may cross 128 VGPRs and silently drop a wave per SIMD.
   if (P.stage == 4096)
-    return launch_t<4096, true, false, false, false, 4, CS, HASH>(P, stream, num_cus);
-  return launch_t<8192, true, false, false, false, 4, CS, HASH>(P, stream, num_cus);
+    return launch_t<4096, true, false, false, false, 4, CS, HASH, 4>(P, stream, num_cus);
+  return launch_t<8192, true, false, false, false, 4, CS, HASH, 2>(P, stream, num_cus);
 }
 
 template <bool EXT, bool PAGES>

@@ -223,6 +223,7 @@ struct gpd_ctx {
     uint32_t *h_status = nullptr, *d_status = nullptr, *h_csum = nullptr, *d_csum = nullptr;
     uint64_t *h_layers = nullptr, *d_layers = nullptr, *h_nh = nullptr, *d_nh = nullptr;
     uint64_t *h_th = nullptr, *d_th = nullptr;
+    uint32_t *h_hoff = nullptr, *d_hoff = nullptr;
     gpd_ext_rec *h_ext = nullptr, *d_ext = nullptr;
     uint64_t lo = 0, hi = 0;  // packet range in flight
     bool busy = false;
@@ -236,6 +237,11 @@ struct gpd_ctx {
     return false;
   }
 };
+
+namespace gpd {
+int ctx_device(const gpd_ctx *ctx) { return ctx->device; }
+int ctx_num_cus(const gpd_ctx *ctx) { return ctx->num_cus; }
+}  // namespace gpd
 
 extern "C" {
 
@@ -349,11 +355,11 @@ static void free_slots(gpd_ctx *ctx) {
     if (s.stream) (void)hipStreamSynchronize(s.stream);
     for (void *p : {(void *)s.h_data, (void *)s.h_off, (void *)s.h_len, (void *)s.h_status,
                     (void *)s.h_csum, (void *)s.h_layers, (void *)s.h_nh, (void *)s.h_th,
-                    (void *)s.h_ext})
+                    (void *)s.h_hoff, (void *)s.h_ext})
       if (p) (void)hipHostFree(p);
     for (void *p : {(void *)s.d_data, (void *)s.d_off, (void *)s.d_len, (void *)s.d_status,
                     (void *)s.d_csum, (void *)s.d_layers, (void *)s.d_nh, (void *)s.d_th,
-                    (void *)s.d_ext})
+                    (void *)s.d_hoff, (void *)s.d_ext})
       if (p) (void)hipFree(p);
     if (s.stream) (void)hipStreamDestroy(s.stream);
     s = gpd_ctx::Slot{};
@@ -425,6 +431,7 @@ static int launch(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, hipS
   P.tp_hash = out->tp_hash;
   P.csum = out->csum;
   P.ext = out->ext;
+  P.hdr_off = out->hdr_off;
   P.image = ctx->d_image;
   P.pages = ctx->d_pages;
   P.image_words = ctx->image_words;
@@ -448,7 +455,8 @@ static int launch(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, hipS
     static const char *d = getenv("GPD_DIAG");
     P.options |= (d ? ((uint32_t)atoi(d) & 3u) : 3u) << 28;
   }
-  P.nstores = 2u + (out->net_hash != nullptr) + (out->tp_hash != nullptr) + (out->csum != nullptr);
+  P.nstores = 2u + (out->net_hash != nullptr) + (out->tp_hash != nullptr) + (out->csum != nullptr) +
+              (out->hdr_off != nullptr);
   if (gpd::fast_eligible(P)) {  // fallback list scratch for this stream, sized for one launch
     const uint64_t need = std::min<uint64_t>(in->n, gpd::kMaxLaunchPackets);
     auto &fb = ctx->fallback[stream];
@@ -479,6 +487,7 @@ static int launch(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, hipS
     Q.tp_hash = out->tp_hash ? out->tp_hash + lo : nullptr;
     Q.csum = out->csum ? out->csum + lo : nullptr;
     Q.ext = out->ext ? out->ext + lo : nullptr;
+    Q.hdr_off = out->hdr_off ? out->hdr_off + lo : nullptr;
     if (gpd::fast_eligible(P)) {  // two counters in their own lines, used alternately: each
       auto &fb = ctx->fallback[stream];  // list kernel zeroes the one the next launch takes
       Q.fb_count = fb.d + 64 * fb.parity;
@@ -533,6 +542,8 @@ static int alloc_slots(gpd_ctx *ctx, uint64_t bytes, uint64_t pkts, bool ext) {
     HIP_TRY(hipMalloc(&s.d_layers, pkts * 8));
     HIP_TRY(hipMalloc(&s.d_nh, pkts * 8));
     HIP_TRY(hipMalloc(&s.d_th, pkts * 8));
+    HIP_TRY(hipHostMalloc(&s.h_hoff, pkts * 4, hipHostMallocDefault));
+    HIP_TRY(hipMalloc(&s.d_hoff, pkts * 4));
     if (ext) {
       HIP_TRY(hipHostMalloc(&s.h_ext, pkts * sizeof(gpd_ext_rec), hipHostMallocDefault));
       HIP_TRY(hipMalloc(&s.d_ext, pkts * sizeof(gpd_ext_rec)));
@@ -550,6 +561,7 @@ static void drain_slot(gpd_ctx::Slot &s, const gpd_result *out) {
   if (out->csum) std::memcpy(out->csum + s.lo, s.h_csum, m * 4);
   if (out->net_hash) std::memcpy(out->net_hash + s.lo, s.h_nh, m * 8);
   if (out->tp_hash) std::memcpy(out->tp_hash + s.lo, s.h_th, m * 8);
+  if (out->hdr_off) std::memcpy(out->hdr_off + s.lo, s.h_hoff, m * 4);
   if (out->ext) std::memcpy(out->ext + s.lo, s.h_ext, m * sizeof(gpd_ext_rec));
   s.busy = false;
 }
@@ -596,7 +608,8 @@ int gpd_decode_host(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out) {
     HIP_TRY(hipMemcpyAsync(s.d_off, s.h_off, m * 4, hipMemcpyHostToDevice, s.stream));
     HIP_TRY(hipMemcpyAsync(s.d_len, s.h_len, m * 4, hipMemcpyHostToDevice, s.stream));
     gpd_batch b{s.d_data, pos, s.d_off, s.d_len, m};
-    gpd_result r{s.d_status, s.d_layers, s.d_nh, s.d_th, s.d_csum, out->ext ? s.d_ext : nullptr};
+    gpd_result r{s.d_status, s.d_layers, s.d_nh, s.d_th, s.d_csum, out->ext ? s.d_ext : nullptr,
+                 out->hdr_off ? s.d_hoff : nullptr};
     rc = launch(ctx, &b, &r, s.stream, false);
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(s.h_status, s.d_status, m * 4, hipMemcpyDeviceToHost, s.stream));
@@ -604,6 +617,8 @@ int gpd_decode_host(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out) {
     if (out->csum) HIP_TRY(hipMemcpyAsync(s.h_csum, s.d_csum, m * 4, hipMemcpyDeviceToHost, s.stream));
     if (out->net_hash) HIP_TRY(hipMemcpyAsync(s.h_nh, s.d_nh, m * 8, hipMemcpyDeviceToHost, s.stream));
     if (out->tp_hash) HIP_TRY(hipMemcpyAsync(s.h_th, s.d_th, m * 8, hipMemcpyDeviceToHost, s.stream));
+    if (out->hdr_off)
+      HIP_TRY(hipMemcpyAsync(s.h_hoff, s.d_hoff, m * 4, hipMemcpyDeviceToHost, s.stream));
     if (out->ext)
       HIP_TRY(hipMemcpyAsync(s.h_ext, s.d_ext, m * sizeof(gpd_ext_rec), hipMemcpyDeviceToHost, s.stream));
     s.lo = i;
@@ -717,7 +732,8 @@ int gpd_decode_pcap(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, uint64_t max
     HIP_TRY(hipMemcpyAsync(s.d_off, s.h_off, m * 4, hipMemcpyHostToDevice, s.stream));
     HIP_TRY(hipMemcpyAsync(s.d_len, s.h_len, m * 4, hipMemcpyHostToDevice, s.stream));
     gpd_batch b{s.d_data, span, s.d_off, s.d_len, m};
-    gpd_result r{s.d_status, s.d_layers, s.d_nh, s.d_th, s.d_csum, nullptr};
+    gpd_result r{s.d_status, s.d_layers, s.d_nh, s.d_th, s.d_csum, nullptr,
+                 out->hdr_off ? s.d_hoff : nullptr};
     rc = launch(ctx, &b, &r, s.stream, false);
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(s.h_status, s.d_status, m * 4, hipMemcpyDeviceToHost, s.stream));
@@ -725,6 +741,8 @@ int gpd_decode_pcap(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, uint64_t max
     if (out->csum) HIP_TRY(hipMemcpyAsync(s.h_csum, s.d_csum, m * 4, hipMemcpyDeviceToHost, s.stream));
     if (out->net_hash) HIP_TRY(hipMemcpyAsync(s.h_nh, s.d_nh, m * 8, hipMemcpyDeviceToHost, s.stream));
     if (out->tp_hash) HIP_TRY(hipMemcpyAsync(s.h_th, s.d_th, m * 8, hipMemcpyDeviceToHost, s.stream));
+    if (out->hdr_off)
+      HIP_TRY(hipMemcpyAsync(s.h_hoff, s.d_hoff, m * 4, hipMemcpyDeviceToHost, s.stream));
     s.lo = i;
     s.hi = j;
     s.busy = true;

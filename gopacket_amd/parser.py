@@ -161,7 +161,7 @@ class DeviceBatch:
 class DeviceResult:
     """Result SoA in HBM; .to_host() gives a BatchResult."""
 
-    def __init__(self, n: int, device: int = 0, ext: bool = False):
+    def __init__(self, n: int, device: int = 0, ext: bool = False, hdr_off: bool = True):
         torch = _torch()
         dev = torch.device("cuda", device)
         self.n = n
@@ -171,18 +171,21 @@ class DeviceResult:
         self.tp_hash = torch.empty(n, dtype=torch.int64, device=dev)
         self.csum = torch.empty(n, dtype=torch.int32, device=dev)
         self.ext = torch.empty(n * EXT_DTYPE.itemsize, dtype=torch.uint8, device=dev) if ext else None
+        self.hdr_off = torch.empty(n, dtype=torch.int32, device=dev) if hdr_off else None
 
     def c_result(self) -> GpdResult:
         return GpdResult(self.status.data_ptr(), self.layers.data_ptr(), self.net_hash.data_ptr(),
                          self.tp_hash.data_ptr(), self.csum.data_ptr(),
-                         self.ext.data_ptr() if self.ext is not None else None)
+                         self.ext.data_ptr() if self.ext is not None else None,
+                         self.hdr_off.data_ptr() if self.hdr_off is not None else None)
 
     def to_host(self) -> BatchResult:
         u = lambda t, dt: t.cpu().numpy().view(dt)
         return BatchResult(u(self.status, np.uint32), u(self.layers, np.uint64),
                            u(self.net_hash, np.uint64), u(self.tp_hash, np.uint64),
                            u(self.csum, np.uint32),
-                           self.ext.cpu().numpy().view(EXT_DTYPE) if self.ext is not None else None)
+                           self.ext.cpu().numpy().view(EXT_DTYPE) if self.ext is not None else None,
+                           u(self.hdr_off, np.uint32) if self.hdr_off is not None else None)
 
 
 class DecodingLayerParser:
@@ -256,12 +259,14 @@ class DecodingLayerParser:
         n = batch.n
         res = out if out is not None else BatchResult(
             np.zeros(n, np.uint32), np.zeros(n, np.uint64), np.zeros(n, np.uint64),
-            np.zeros(n, np.uint64), np.zeros(n, np.uint32), np.zeros(n, EXT_DTYPE) if ext else None)
+            np.zeros(n, np.uint64), np.zeros(n, np.uint32), np.zeros(n, EXT_DTYPE) if ext else None,
+            np.zeros(n, np.uint32))
         b = GpdBatch(batch.data.ctypes.data, batch.data_len, batch.offset.ctypes.data,
                      batch.caplen.ctypes.data, n)
         r = GpdResult(res.status.ctypes.data, res.layers.ctypes.data, res.net_hash.ctypes.data,
                       res.tp_hash.ctypes.data, res.csum.ctypes.data,
-                      res.ext.ctypes.data if ext else None)
+                      res.ext.ctypes.data if res.ext is not None else None,
+                      res.hdr_off.ctypes.data if res.hdr_off is not None else None)
         check(lib.gpd_decode_host(self.ctx().h, C.byref(b), C.byref(r)), "gpd_decode_host")
         return res
 
@@ -274,9 +279,10 @@ class DecodingLayerParser:
         dl = cap.shape[0] - PAD if data_len is None else int(data_len)
         m = (dl - 24) // 16 + 1 if max_n is None else int(max_n)
         res = BatchResult(np.zeros(m, np.uint32), np.zeros(m, np.uint64), np.zeros(m, np.uint64),
-                          np.zeros(m, np.uint64), np.zeros(m, np.uint32), None)
+                          np.zeros(m, np.uint64), np.zeros(m, np.uint32), None,
+                          np.zeros(m, np.uint32))
         r = GpdResult(res.status.ctypes.data, res.layers.ctypes.data, res.net_hash.ctypes.data,
-                      res.tp_hash.ctypes.data, res.csum.ctypes.data, None)
+                      res.tp_hash.ctypes.data, res.csum.ctypes.data, None, res.hdr_off.ctypes.data)
         n, nxt, stop = C.c_uint64(), C.c_uint64(), C.c_int()
         rc = lib.gpd_decode_pcap(self.ctx().h, cap.ctypes.data, dl, m, C.byref(r), C.byref(n),
                                  C.byref(nxt), C.byref(stop), int(nthreads))
@@ -287,7 +293,7 @@ class DecodingLayerParser:
             check(rc, "gpd_decode_pcap")
         k = n.value
         out = BatchResult(res.status[:k], res.layers[:k], res.net_hash[:k], res.tp_hash[:k],
-                          res.csum[:k], None)
+                          res.csum[:k], None, res.hdr_off[:k])
         return out, k, err
 
     def DecodeLayers(self, data: bytes, decoded: list):

@@ -53,6 +53,7 @@ class BatchResult:
     tp_hash: Optional[np.ndarray] = None
     csum: Optional[np.ndarray] = None
     ext: Optional[np.ndarray] = None  # EXT_DTYPE[n]
+    hdr_off: Optional[np.ndarray] = None  # uint32[n], gpd.h header offsets word
 
     def __len__(self):
         return int(self.status.shape[0])
@@ -107,6 +108,16 @@ class BatchResult:
         s = int(self.status[i])
         return int(self.csum[i]) >> 16 if (s >> 19) & 1 else None
 
+    def network_offset(self, i: int) -> Optional[int]:
+        """Offset of the layer NetworkFlow() reads (the last IPv4/IPv6), or None."""
+        h = int(self.hdr_off[i]) & 0xFFFF
+        return None if h == 0xFFFF else h
+
+    def transport_offset(self, i: int) -> Optional[int]:
+        """Offset of the layer TransportFlow() reads (the last TCP/UDP), or None."""
+        h = int(self.hdr_off[i]) >> 16
+        return None if h == 0xFFFF else h
+
     def layer(self, i: int, name: str):
         """(contents, payload) byte ranges of a layer object after the call, or None."""
         if self.ext is None:
@@ -122,4 +133,4 @@ class BatchResult:
 def empty_result(n: int, ext: bool = False) -> BatchResult:
     return BatchResult(np.zeros(n, np.uint32), np.zeros(n, np.uint64), np.zeros(n, np.uint64),
                        np.zeros(n, np.uint64), np.zeros(n, np.uint32),
-                       np.zeros(n, EXT_DTYPE) if ext else None)
+                       np.zeros(n, EXT_DTYPE) if ext else None, np.zeros(n, np.uint32))

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define GPD_ABI_VERSION 2  /* 2: ICMPv4 + LLC decoders, 12 objects, 224-B ext record */
+#define GPD_ABI_VERSION 3  /* 2: ICMPv4 + LLC, 12 objects, 224-B ext; 3: gpd_result.hdr_off */
 
 /* ---- gopacket LayerType numbers (layertypes.go:14-154, decode.go:105-116) ---- */
 #define GPD_LT_ZERO            0
@@ -102,8 +102,10 @@ extern "C" {
  *  [17]    tp_hash valid    (a TCP/UDP layer is in decoded)
  *  [18]    IPv4 header checksum valid (IPv4 in decoded)
  *  [19]    L4 checksum valid (TCP/UDP in decoded, preceded by IPv4/IPv6)
- *  [23:20] network EndpointType of net_hash (1 IPv4, 2 IPv6; layers/endpoints.go:20-23)
- *  [27:24] transport EndpointType of tp_hash (4 TCP, 5 UDP; layers/endpoints.go:29-32)
+ *  [23:20] EndpointType of NetworkFlow(): of the last IPv4/IPv6 in decoded (1 IPv4, 2 IPv6,
+ *          0 none; layers/endpoints.go:20-23), whether or not hashes are computed
+ *  [27:24] EndpointType of TransportFlow(): of the last TCP/UDP (4 TCP, 5 UDP, 0 none;
+ *          layers/endpoints.go:29-32)
  *  [31:28] reserved (0)                                                          */
 #define GPD_ST_OK            0u
 #define GPD_ST_UNSUPPORTED   1u
@@ -249,6 +251,17 @@ typedef struct gpd_batch {
   uint64_t        n;
 } gpd_batch;
 
+/* ---- header offsets word (uint32): where the flows' layers sit in the packet ----
+ *  [15:0]  offset (from the packet start) of the network layer NetworkFlow() reads: the
+ *          last IPv4/IPv6 in decoded (ip4/ip6.Contents[0]); 0xFFFF if none
+ *  [31:16] offset of the transport layer TransportFlow() reads: the last TCP/UDP in
+ *          decoded; 0xFFFF if none
+ * Offsets >= 0xFFFF saturate to 0xFFFF.  With these a caller fills the layer structs (or
+ * builds the [2]Flow key tcpassembly uses) straight from the packet bytes, zero copy. */
+#define GPD_HDR_NET(h) ((uint32_t)((h) & 0xFFFFu))
+#define GPD_HDR_TP(h)  ((uint32_t)((h) >> 16))
+#define GPD_HDR_NONE   0xFFFFu
+
 /* ---- results (caller-allocated SoA, n entries each) ----
  * status and layers are required; the others may be NULL (not written). */
 typedef struct gpd_result {
@@ -258,6 +271,7 @@ typedef struct gpd_result {
   uint64_t    *tp_hash;    /* tcp/udp.TransportFlow().FastHash() */
   uint32_t    *csum;
   gpd_ext_rec *ext;
+  uint32_t    *hdr_off;    /* header offsets word (above) */
 } gpd_result;
 
 typedef struct gpd_ctx gpd_ctx;

@@ -1,0 +1,94 @@
+/*
+ * gpd_flow.h — C-ABI of the GPU flow table behind the batched decoder.
+ *
+ * The reference's immediate consumer of decoded packets is the stream assembler, which keys
+ * every TCP packet by the pair [2]gopacket.Flow{NetworkFlow(), TransportFlow()} and finds or
+ * creates the connection for that key in a Go map (tcpassembly/assembly.go:289 `type key
+ * [2]gopacket.Flow`, :311 `conns map[key]*connection`, :495-511 getConnection, :543 the key
+ * built from a packet; reassembly/tcpassembly.go:389,644).  Flow equality is struct
+ * equality: EndpointType, both lengths, and the raw bytes zero-padded to 16 (flows.go:140-146,
+ * NewFlow :214-224).
+ * Here the same find-or-create runs for a whole decoded batch in HBM: every packet whose
+ * decode left both a network and a transport layer (TCP or UDP) is looked up by its exact
+ * key; a new key creates a flow record; each packet gets the index of its flow record.
+ *
+ * Reference interfaces each entry point replaces (paths relative to google/gopacket):
+ *   gpd_flow_create   tcpassembly.NewStreamPool and the `conns map[key]*connection` it holds
+ *                                                        tcpassembly/assembly.go:305-343
+ *   gpd_flow_insert   StreamPool.getConnection(k, ...) for every packet of a batch, with
+ *                     k = key{netFlow, t.TransportFlow()} as AssembleWithTimestamp builds it
+ *                                                        tcpassembly/assembly.go:495-511,533-543;
+ *                                                        reassembly/tcpassembly.go:644
+ *   gpd_flow_export   iterating the pool's connections (StreamPool.connections,
+ *                     tcpassembly/assembly.go:193-200)
+ *   gpd_flow_reset / gpd_flow_destroy                    (pool lifetime)
+ *
+ * The table is open addressing in HBM: 2^k records of 80 bytes; a record is claimed by a
+ * 64-bit fingerprint of its key with one compare-and-swap, then every packet's full key is
+ * compared with the record's stored key in a second pass, so a fingerprint collision is
+ * detected (counted in gpd_flow_stats.collisions, the packet's flow id flagged) rather than
+ * merging two flows silently.
+ */
+#ifndef GPD_FLOW_H_
+#define GPD_FLOW_H_
+#include "gpd.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* One flow record (80 B, device memory; gpd_flow_export copies occupied ones out). */
+typedef struct gpd_flow_rec {
+  uint64_t fp;          /* key fingerprint; 0 = empty record */
+  uint8_t  src[16];     /* NetworkFlow().Src() raw bytes (4 used for IPv4) */
+  uint8_t  dst[16];     /* NetworkFlow().Dst() raw bytes */
+  uint8_t  sport[2];    /* TransportFlow().Src() raw bytes (big-endian port) */
+  uint8_t  dport[2];    /* TransportFlow().Dst() raw bytes */
+  uint8_t  net_type;    /* EndpointType of the network flow: 1 IPv4, 2 IPv6 */
+  uint8_t  tp_type;     /* EndpointType of the transport flow: 4 TCP, 5 UDP */
+  uint8_t  addr_len;    /* 4 or 16 */
+  uint8_t  reserved;
+  uint64_t first;       /* lowest packet sequence number (index_base + i) of the flow */
+  uint64_t packets;     /* packets of the flow */
+  uint64_t bytes;       /* sum of their captured lengths */
+  uint64_t last;        /* highest packet sequence number */
+} gpd_flow_rec;
+
+/* flow_id[i] values besides a record index */
+#define GPD_FLOW_NONE       0xFFFFFFFFu  /* packet has no network + transport layer pair */
+#define GPD_FLOW_FULL       0xFFFFFFFEu  /* no free record found (table full) */
+#define GPD_FLOW_COLLISION  0x80000000u  /* OR-ed into the id: fingerprint matched, key did not */
+
+typedef struct gpd_flow_stats {
+  uint64_t flows;        /* records in use */
+  uint64_t packets;      /* packets assigned to a flow (all inserts since the last reset) */
+  uint64_t no_key;       /* packets without a network + transport pair */
+  uint64_t full;         /* packets that found no free record */
+  uint64_t collisions;   /* packets whose fingerprint matched another key (should stay 0) */
+  uint64_t capacity;     /* records in the table */
+} gpd_flow_stats;
+
+typedef struct gpd_flowtable gpd_flowtable;
+
+/* A table of at least `capacity` records (rounded up to a power of two) on ctx's device. */
+int gpd_flow_create(gpd_ctx *ctx, uint64_t capacity, gpd_flowtable **out);
+/* Empty the table (asynchronous on `stream`). */
+int gpd_flow_reset(gpd_flowtable *ft, void *stream);
+/* Find-or-create the flow of every packet of a decoded batch (device pointers): `in` is the
+ * batch gpd_decode read, `res` its results (status and hdr_off required), flow_id[n] receives
+ * each packet's record index (or a GPD_FLOW_* value).  Packet i counts as sequence number
+ * index_base + i.  Asynchronous on `stream`; the batch must be decoded on that stream first. */
+int gpd_flow_insert(gpd_flowtable *ft, const gpd_batch *in, const gpd_result *res,
+                    uint32_t *flow_id, uint64_t index_base, void *stream);
+/* Counters since the last reset (synchronises `stream`). */
+int gpd_flow_stats_get(gpd_flowtable *ft, gpd_flow_stats *out, void *stream);
+/* Copy up to max occupied records to host memory, ordered by `first` (synchronises
+ * `stream`); *n = number copied.  rec_index (may be NULL) receives each one's index. */
+int gpd_flow_export(gpd_flowtable *ft, gpd_flow_rec *out, uint32_t *rec_index, uint64_t max,
+                    uint64_t *n, void *stream);
+int gpd_flow_destroy(gpd_flowtable *ft);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPD_FLOW_H_ */

@@ -421,7 +421,7 @@ uint64_t gpo_endpoint_fasthash(uint32_t ept, const uint8_t *raw, uint32_t len) {
 void gpo_decode_packet(const uint8_t *pkt, uint32_t caplen, uint32_t first, uint32_t mask,
                        uint32_t options, const gpo_tables *t, uint32_t *status_out,
                        uint64_t *layers_out, uint64_t *net_hash_out, uint64_t *tp_hash_out,
-                       uint32_t *csum_out, gpd_ext_rec *ext) {
+                       uint32_t *csum_out, uint32_t *hdr_off_out, gpd_ext_rec *ext) {
   st s;
   memset(&s, 0, sizeof s);
   s.pkt = pkt;
@@ -488,17 +488,21 @@ void gpo_decode_packet(const uint8_t *pkt, uint32_t caplen, uint32_t first, uint
 
   uint64_t nh = 0, th = 0;
   uint32_t csum = 0;
+  /* EndpointTypes of the flows' layers (layers/endpoints.go:20-32), hashed or not */
+  if (last_net >= 0) status |= (last_net == GPD_OBJ_IPV4 ? 1u : 2u) << 20;
+  if (last_tp >= 0) status |= (last_tp == GPD_OBJ_TCP ? 4u : 5u) << 24;
   if (!(options & GPD_OPT_NO_FLOW_HASH)) {
     if (last_net >= 0) {
       const uint8_t *c = pkt + obj[last_net].contents_off;
-      if (last_net == GPD_OBJ_IPV4) { nh = gpo_flow_fasthash(1, c + 12, 4, c + 16, 4); status |= (1u << 16) | (1u << 20); }
-      else { nh = gpo_flow_fasthash(2, c + 8, 16, c + 24, 16); status |= (1u << 16) | (2u << 20); }
+      if (last_net == GPD_OBJ_IPV4) nh = gpo_flow_fasthash(1, c + 12, 4, c + 16, 4);
+      else nh = gpo_flow_fasthash(2, c + 8, 16, c + 24, 16);
+      status |= 1u << 16;
     }
     if (last_tp >= 0) {
       const uint8_t *c = pkt + obj[last_tp].contents_off;
       uint32_t ept = last_tp == GPD_OBJ_TCP ? 4 : 5;
       th = gpo_flow_fasthash(ept, c, 2, c + 2, 2);
-      status |= (1u << 17) | (ept << 24);
+      status |= 1u << 17;
     }
   }
   if (!(options & GPD_OPT_NO_CHECKSUMS)) {
@@ -528,6 +532,11 @@ void gpo_decode_packet(const uint8_t *pkt, uint32_t caplen, uint32_t first, uint
   if (net_hash_out) *net_hash_out = nh;
   if (tp_hash_out) *tp_hash_out = th;
   if (csum_out) *csum_out = csum;
+  if (hdr_off_out) { /* gpd.h header offsets word: the objects NetworkFlow/TransportFlow read */
+    uint32_t a = last_net >= 0 ? obj[last_net].contents_off : 0xFFFFu;
+    uint32_t b = last_tp >= 0 ? obj[last_tp].contents_off : 0xFFFFu;
+    *hdr_off_out = (a < 0xFFFFu ? a : 0xFFFFu) | ((b < 0xFFFFu ? b : 0xFFFFu) << 16);
+  }
   if (ext) {
     memset(ext, 0, sizeof *ext);
     ext->layer_codes[0] = ext_codes[0];
@@ -546,7 +555,8 @@ typedef struct {
   uint64_t lo, hi;
   uint32_t first, decoders, options;
   const gpo_tables *t;
-  uint32_t *status; uint64_t *layers, *net_hash, *tp_hash; uint32_t *csum; gpd_ext_rec *ext;
+  uint32_t *status; uint64_t *layers, *net_hash, *tp_hash; uint32_t *csum, *hdr_off;
+  gpd_ext_rec *ext;
 } job;
 
 static void run_job(const job *j) {
@@ -554,7 +564,8 @@ static void run_job(const job *j) {
     gpo_decode_packet(j->data + j->offset[i], j->caplen[i], j->first, j->decoders, j->options,
                       j->t, &j->status[i], &j->layers[i],
                       j->net_hash ? &j->net_hash[i] : 0, j->tp_hash ? &j->tp_hash[i] : 0,
-                      j->csum ? &j->csum[i] : 0, j->ext ? &j->ext[i] : 0);
+                      j->csum ? &j->csum[i] : 0, j->hdr_off ? &j->hdr_off[i] : 0,
+                      j->ext ? &j->ext[i] : 0);
   }
 }
 
@@ -564,14 +575,14 @@ void gpo_decode_batch(const uint8_t *data, const uint32_t *offset, const uint32_
                       uint64_t n, uint32_t first, uint32_t decoders, uint32_t options,
                       const gpo_tables *t, uint32_t *status, uint64_t *layers,
                       uint64_t *net_hash, uint64_t *tp_hash, uint32_t *csum,
-                      gpd_ext_rec *ext, int nthreads) {
+                      uint32_t *hdr_off, gpd_ext_rec *ext, int nthreads) {
   if (nthreads < 1) nthreads = 1;
   if (nthreads > 256) nthreads = 256;
   job jobs[256];
   pthread_t th[256];
   for (int k = 0; k < nthreads; k++) {
     job j = {data, offset, caplen, n * k / nthreads, n * (k + 1) / nthreads,
-             first, decoders, options, t, status, layers, net_hash, tp_hash, csum, ext};
+             first, decoders, options, t, status, layers, net_hash, tp_hash, csum, hdr_off, ext};
     jobs[k] = j;
   }
   if (nthreads == 1) { run_job(&jobs[0]); return; }

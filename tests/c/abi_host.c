@@ -41,7 +41,7 @@
   } while (0)
 
 typedef struct {
-  uint32_t *status, *csum;
+  uint32_t *status, *csum, *hdr_off;
   uint64_t *layers, *net_hash, *tp_hash;
 } res_t;
 
@@ -49,6 +49,7 @@ static res_t res_alloc(uint64_t n) {
   res_t r;
   r.status = calloc(n, 4);
   r.csum = calloc(n, 4);
+  r.hdr_off = calloc(n, 4);
   r.layers = calloc(n, 8);
   r.net_hash = calloc(n, 8);
   r.tp_hash = calloc(n, 8);
@@ -59,7 +60,7 @@ static int res_cmp(const char *what, const res_t *a, const res_t *b, uint64_t n)
   for (uint64_t i = 0; i < n; i++) {
     if (a->status[i] != b->status[i] || a->layers[i] != b->layers[i] ||
         a->net_hash[i] != b->net_hash[i] || a->tp_hash[i] != b->tp_hash[i] ||
-        a->csum[i] != b->csum[i]) {
+        a->csum[i] != b->csum[i] || a->hdr_off[i] != b->hdr_off[i]) {
       fprintf(stderr,
               "%s: packet %llu differs: status %08x/%08x layers %016llx/%016llx net %016llx/%016llx "
               "tp %016llx/%016llx csum %08x/%08x\n",
@@ -106,7 +107,7 @@ int main(int argc, char **argv) {
 
   /* 1. device-resident batch on the caller's stream */
   res_t dv = res_alloc(n);
-  void *d_data, *d_off, *d_cap, *d_st, *d_ly, *d_nh, *d_th, *d_cs;
+  void *d_data, *d_off, *d_cap, *d_st, *d_ly, *d_nh, *d_th, *d_cs, *d_ho;
   hipStream_t s;
   HCHECK(hipStreamCreate(&s));
   HCHECK(hipMalloc(&d_data, alloc));
@@ -117,13 +118,14 @@ int main(int argc, char **argv) {
   HCHECK(hipMalloc(&d_nh, 8 * n + 8));
   HCHECK(hipMalloc(&d_th, 8 * n + 8));
   HCHECK(hipMalloc(&d_cs, 4 * n + 4));
+  HCHECK(hipMalloc(&d_ho, 4 * n + 4));
   HCHECK(hipMemcpy(d_data, data, alloc, hipMemcpyHostToDevice));
   HCHECK(hipMemcpy(d_off, off, 4 * n, hipMemcpyHostToDevice));
   HCHECK(hipMemcpy(d_cap, cap, 4 * n, hipMemcpyHostToDevice));
   gpd_batch db = {(const uint8_t *)d_data, data_len, (const uint32_t *)d_off,
                   (const uint32_t *)d_cap, n};
   gpd_result dr = {(uint32_t *)d_st, (uint64_t *)d_ly, (uint64_t *)d_nh, (uint64_t *)d_th,
-                   (uint32_t *)d_cs, NULL};
+                   (uint32_t *)d_cs, NULL, (uint32_t *)d_ho};
   CHECK(gpd_decode(ctx, &db, &dr, s));
   CHECK(gpd_sync(ctx, s));
   HCHECK(hipMemcpy(dv.status, d_st, 4 * n, hipMemcpyDeviceToHost));
@@ -131,11 +133,12 @@ int main(int argc, char **argv) {
   HCHECK(hipMemcpy(dv.net_hash, d_nh, 8 * n, hipMemcpyDeviceToHost));
   HCHECK(hipMemcpy(dv.tp_hash, d_th, 8 * n, hipMemcpyDeviceToHost));
   HCHECK(hipMemcpy(dv.csum, d_cs, 4 * n, hipMemcpyDeviceToHost));
+  HCHECK(hipMemcpy(dv.hdr_off, d_ho, 4 * n, hipMemcpyDeviceToHost));
 
   /* 2. host batch through the library's pinned pipeline */
   res_t hv = res_alloc(n);
   gpd_batch hb = {data, data_len, off, cap, n};
-  gpd_result hr = {hv.status, hv.layers, hv.net_hash, hv.tp_hash, hv.csum, NULL};
+  gpd_result hr = {hv.status, hv.layers, hv.net_hash, hv.tp_hash, hv.csum, NULL, hv.hdr_off};
   CHECK(gpd_decode_host(ctx, &hb, &hr));
 
   /* 3. the oracle */
@@ -145,7 +148,7 @@ int main(int argc, char **argv) {
   gpd_default_tables(et, ip, tp, up);
   gpo_tables t = {et, ip, tp, up};
   gpo_decode_batch(data, off, cap, n, GPD_LT_ETHERNET, cfg.decoders, cfg.options, &t, ov.status,
-                   ov.layers, ov.net_hash, ov.tp_hash, ov.csum, NULL, 8);
+                   ov.layers, ov.net_hash, ov.tp_hash, ov.csum, ov.hdr_off, NULL, 8);
 
   int bad = res_cmp("gpd_decode vs oracle", &dv, &ov, n) | res_cmp("gpd_decode_host vs oracle", &hv, &ov, n);
   CHECK(gpd_ctx_destroy(ctx));

@@ -40,7 +40,7 @@ def lib():
         L.gpo_decode_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32,
                                        C.c_uint32, C.c_uint32, C.POINTER(_Tables), C.c_void_p,
                                        C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
-                                       C.c_int]
+                                       C.c_void_p, C.c_int]
         L.gpo_ip4_header_checksum.restype = C.c_uint16
         L.gpo_ip4_header_checksum.argtypes = [C.c_char_p, C.c_uint32]
         L.gpo_tcpip_checksum.restype = C.c_uint16
@@ -68,9 +68,10 @@ def decode(batch, first: int = 17, decoders: int = 0x3FF, options: int = 0,
     n = batch.n
     res = BatchResult(np.zeros(n, np.uint32), np.zeros(n, np.uint64), np.zeros(n, np.uint64),
                       np.zeros(n, np.uint64), np.zeros(n, np.uint32),
-                      np.zeros(n, EXT_DTYPE) if ext else None)
+                      np.zeros(n, EXT_DTYPE) if ext else None, np.zeros(n, np.uint32))
     lib().gpo_decode_batch(batch.data.ctypes.data, batch.offset.ctypes.data, batch.caplen.ctypes.data,
                            n, first, decoders, options, C.byref(tabs), res.status.ctypes.data,
                            res.layers.ctypes.data, res.net_hash.ctypes.data, res.tp_hash.ctypes.data,
-                           res.csum.ctypes.data, res.ext.ctypes.data if ext else None, nthreads)
+                           res.csum.ctypes.data, res.hdr_off.ctypes.data,
+                           res.ext.ctypes.data if ext else None, nthreads)
     return res

@@ -12,7 +12,7 @@ import pytest
 
 from conftest import ROOT, gpu_available
 
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("gpd.h", "gpd_pcap.h")]
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("gpd.h", "gpd_pcap.h", "gpd_flow.h")]
 
 
 def declared_functions():
@@ -26,7 +26,8 @@ def test_header_declares_the_boundary():
     fns = declared_functions()
     for f in ("gpd_ctx_create", "gpd_decode", "gpd_decode_host", "gpd_sync", "gpd_ctx_destroy",
               "gpd_last_error_string", "gpd_ctx_reload_tables", "gpd_default_tables",
-              "gpd_pcap_header", "gpd_pcap_index", "gpd_decode_pcap", "gpd_host_register"):
+              "gpd_pcap_header", "gpd_pcap_index", "gpd_decode_pcap", "gpd_host_register",
+              "gpd_flow_create", "gpd_flow_insert", "gpd_flow_export", "gpd_flow_stats_get"):
         assert f in fns
 
 
@@ -35,7 +36,7 @@ def test_library_exports_every_declared_symbol():
     lib = C.CDLL(_lib.LIB_PATH)
     missing = [f for f in declared_functions() if not hasattr(lib, f)]
     assert not missing, missing
-    assert lib.gpd_abi_version() == 2
+    assert lib.gpd_abi_version() == 3
 
 
 def test_python_binding_covers_the_header():
@@ -59,15 +60,21 @@ def test_struct_layouts_match_c(tmp_path):
     from gopacket_amd import _lib
     from gopacket_amd.results import EXT_DTYPE
     prog = tmp_path / "sz.c"
-    prog.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "gpd_pcap.h"\nint main(void){'
-                    'printf("%zu %zu %zu %zu %zu %zu %zu\\n", sizeof(gpd_config), sizeof(gpd_batch),'
+    prog.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "gpd_pcap.h"\n#include "gpd_flow.h"\n'
+                    'int main(void){'
+                    'printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(gpd_config), sizeof(gpd_batch),'
                     ' sizeof(gpd_result), sizeof(gpd_ext_rec), offsetof(gpd_ext_rec, obj),'
-                    ' sizeof(gpd_layer_rec), sizeof(gpd_pcap_info)); return 0;}\n')
+                    ' sizeof(gpd_layer_rec), sizeof(gpd_pcap_info), sizeof(gpd_flow_rec),'
+                    ' offsetof(gpd_flow_rec, net_type), offsetof(gpd_flow_rec, first), sizeof(gpd_flow_stats));'
+                    ' return 0;}\n')
     exe = tmp_path / "sz"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(prog), "-o", str(exe)], check=True)
     out = list(map(int, subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()))
+    from gopacket_amd.flows import FLOW_REC_DTYPE, FlowStats
     assert out == [C.sizeof(_lib.GpdConfig), C.sizeof(_lib.GpdBatch), C.sizeof(_lib.GpdResult),
-                   EXT_DTYPE.itemsize, EXT_DTYPE.fields["obj"][1], 16, C.sizeof(_lib.GpdPcapInfo)]
+                   EXT_DTYPE.itemsize, EXT_DTYPE.fields["obj"][1], 16, C.sizeof(_lib.GpdPcapInfo),
+                   FLOW_REC_DTYPE.itemsize, FLOW_REC_DTYPE.fields["net_type"][1],
+                   FLOW_REC_DTYPE.fields["first"][1], C.sizeof(FlowStats)]
 
 
 @pytest.mark.skipif(gpu_available(), reason="checks the no-device error path")

@@ -34,8 +34,10 @@ def _parser(first=L.LayerTypeEthernet, mask=ALL, options=0, tables=None):
 
 
 def assert_same(dev, ref, batch=None, ext=True):
-    for f in ("status", "layers", "net_hash", "tp_hash", "csum"):
+    for f in ("status", "layers", "net_hash", "tp_hash", "csum", "hdr_off"):
         a, b = getattr(dev, f), getattr(ref, f)
+        if a is None or b is None:
+            continue
         bad = np.nonzero(a != b)[0]
         if len(bad):
             i = int(bad[0])

@@ -40,7 +40,7 @@ def main():
     lib.gpd_diag_phase.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
     _, n = bench.CONFIGS[a.config]
     batch = bench.make_batch(a.config, n, 0)
-    db, dr = P.DeviceBatch(batch, 0), P.DeviceResult(n, 0, ext=False)
+    db, dr = P.DeviceBatch(batch, 0), P.DeviceResult(n, 0, ext=False, hdr_off=False)
     p = P.NewDecodingLayerParser(L.LayerTypeEthernet, P.Ethernet(), P.Dot1Q(), P.IPv4(), P.IPv6(),
                                  P.IPv6ExtensionSkipper(), P.TCP(), P.UDP(), P.VXLAN(), P.Payload(),
                                  P.Fragment(), device=0)
