@@ -181,6 +181,38 @@ def bench_flows(parser, dev_batch, n, args, stream, local):
             "collisions": st["collisions"], "full": st["full"]}
 
 
+def bench_tpv3(parser, batch, args):
+    """F2 diagnostic: the config's first packets laid out as the kernel fills a TPACKET_V3
+    ring (1 MiB blocks, 256 of them), host-registered like a pinned socket ring, then
+    gpd_decode_tpv3 (native block walk, H2D of the blocks, decode in place, D2H of the
+    results) timed on the host clock.  PCIe-inclusive; never the metric."""
+    from gopacket_amd import afpacket as A
+    from gopacket_amd import synth
+    from gopacket_amd._lib import check, lib
+    bs, nb = 1 << 20, 256
+    per = bs // (((82 + int(batch.caplen.max())) + 15) // 16 * 16) - 1
+    m = min(batch.n, per * nb)
+    arr, used = synth.make_tpv3_ring([batch.packet(i) for i in range(m)], bs, nb)
+    ring = A.TPv3Ring(arr, bs, nb)
+    check(lib.gpd_host_register(parser.ctx().h, arr.ctypes.data, arr.nbytes), "gpd_host_register")
+    try:
+        parser.DecodeTPv3(ring, max_n=m)  # warm
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            res, ci, nblk = parser.DecodeTPv3(ring, max_n=m)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el > 3 or reps >= 20:
+                break
+    finally:
+        lib.gpd_host_unregister(parser.ctx().h, arr.ctypes.data)
+    assert len(res) == m and nblk == len(used)
+    return {"diag": "F2 TPACKET_V3 ring walk + decode (PCIe-inclusive, not the metric)",
+            "packets": m, "blocks": nblk, "block_size": bs, "ring_bytes": int(arr.nbytes),
+            "ms_per_ring": round(el / reps * 1e3, 3), "Mpackets_per_s": round(m * reps / el / 1e6, 1),
+            "GBps_ring_in": round(len(used) * bs * reps / el / 1e9, 2)}
+
+
 def replay_pcap(parser, cap, n, total, threads):
     """PCIe-inclusive rate: the capture in (registered) host memory replayed through
     gpd_decode_pcap — native index, raw capture bytes H2D, decode, results D2H — until `total`
@@ -224,6 +256,9 @@ def main():
     ap.add_argument("--flows", action="store_true",
                     help="diagnostic: also time the F3 flow table (gpd_flow_insert) on the decoded "
                     "batch; printed as a separate line, never the reported metric")
+    ap.add_argument("--tpv3", action="store_true",
+                    help="diagnostic: walk + decode a TPACKET_V3 ring of the config's packets "
+                    "(gpd_decode_tpv3, PCIe-inclusive); printed as a separate line")
     ap.add_argument("--ablate", default="", help="diagnostics only: 'nocsum', 'nohash' or both "
                     "(comma separated); never used for the reported metric")
     args = ap.parse_args()
@@ -355,6 +390,8 @@ def main():
         out["cpu_baseline"] = cpu_baseline(batch, args.cpu_budget)
     if rank == 0:
         print(json.dumps(out), flush=True)
+    if args.tpv3 and rank == 0:
+        print(json.dumps(bench_tpv3(parser, batch, args)), flush=True)
     if args.flows and rank == 0:
         print(json.dumps(bench_flows(parser, dev_batch, n, args, stream, local)), flush=True)
     if dist:

@@ -72,6 +72,13 @@ EXPORTS = {
     "gpd_flow_export": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
                                   C.POINTER(C.c_uint64), C.c_void_p]),
     "gpd_flow_destroy": (C.c_int, [C.c_void_p]),
+    # include/gpd_afpacket.h
+    "gpd_tpv3_walk": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64, C.c_void_p,
+                                C.POINTER(C.c_uint64), C.POINTER(C.c_uint32), C.c_int]),
+    "gpd_tpv3_release": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32]),
+    "gpd_decode_tpv3": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_int,
+                                  C.c_uint64, C.POINTER(GpdResult), C.c_void_p,
+                                  C.POINTER(C.c_uint64), C.POINTER(C.c_uint32), C.c_int]),
 }
 
 GPD_ERR_PCAP = -5

@@ -92,6 +92,9 @@ int set_error(int code, const char *fmt, ...);
 // Host side: the device and compute-unit count of a context (gpd_runtime.cpp).
 int ctx_device(const gpd_ctx *ctx);
 int ctx_num_cus(const gpd_ctx *ctx);
+// Host side: device scratch buffer `slot` (0..15) of at least `bytes`, kept with the context
+// and grown on demand; nullptr when out of memory.  Callers synchronise before reuse.
+void *ctx_scratch(gpd_ctx *ctx, int slot, size_t bytes);
 
 // Host side: the sequential pcap record walk over buf[pos:len), built in parallel
 // (gpd_pcap.cpp; semantics in include/gpd_pcap.h).  Positions are record-header offsets.

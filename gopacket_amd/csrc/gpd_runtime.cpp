@@ -212,6 +212,11 @@ struct gpd_ctx {
     uint32_t parity = 0;
   };
   std::map<hipStream_t, Fallback> fallback;
+  // device scratch that grows on demand and lives with the context (ctx_scratch)
+  struct Scratch {
+    void *d = nullptr;
+    size_t bytes = 0;
+  } scratch[16];
   bool timing = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
@@ -241,6 +246,19 @@ struct gpd_ctx {
 namespace gpd {
 int ctx_device(const gpd_ctx *ctx) { return ctx->device; }
 int ctx_num_cus(const gpd_ctx *ctx) { return ctx->num_cus; }
+void *ctx_scratch(gpd_ctx *ctx, int slot, size_t bytes) {
+  if (slot < 0 || slot >= 16) return nullptr;
+  auto &sc = ctx->scratch[slot];
+  if (sc.bytes < bytes) {
+    if (sc.d) (void)hipFree(sc.d);
+    sc.d = nullptr;
+    sc.bytes = 0;
+    const size_t want = bytes + bytes / 4;  // headroom: a slightly larger walk reuses it
+    if (hipMalloc(&sc.d, want) != hipSuccess) return nullptr;
+    sc.bytes = want;
+  }
+  return sc.d;
+}
 }  // namespace gpd
 
 extern "C" {
@@ -375,6 +393,8 @@ int gpd_ctx_destroy(gpd_ctx *ctx) {
   if (ctx->d_pages) (void)hipFree(ctx->d_pages);
   for (auto &kv : ctx->fallback)
     if (kv.second.d) (void)hipFree(kv.second.d);
+  for (auto &sc : ctx->scratch)
+    if (sc.d) (void)hipFree(sc.d);
   for (const auto &r : ctx->registered) (void)hipHostUnregister((void *)r.first);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);

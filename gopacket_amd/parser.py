@@ -296,6 +296,29 @@ class DecodingLayerParser:
                           res.csum[:k], None, res.hdr_off[:k])
         return out, k, err
 
+    def DecodeTPv3(self, ring, max_n: int = 1 << 20, max_blocks: Optional[int] = None,
+                   add_vlan_header: bool = False, nthreads: int = 0):
+        """Every packet of the user-owned blocks of a TPACKET_V3 ring (afpacket.TPv3Ring) from
+        ring.offset on, decoded on the GPU where it lies (gpd_decode_tpv3).  The blocks are not
+        released.  Returns (BatchResult, CaptureInfo, blocks walked)."""
+        from .afpacket import CaptureInfo
+        ci = CaptureInfo.alloc(max_n)
+        res = BatchResult(np.zeros(max_n, np.uint32), np.zeros(max_n, np.uint64),
+                          np.zeros(max_n, np.uint64), np.zeros(max_n, np.uint64),
+                          np.zeros(max_n, np.uint32), None, np.zeros(max_n, np.uint32))
+        r = GpdResult(res.status.ctypes.data, res.layers.ctypes.data, res.net_hash.ctypes.data,
+                      res.tp_hash.ctypes.data, res.csum.ctypes.data, None, res.hdr_off.ctypes.data)
+        n, nb = C.c_uint64(), C.c_uint32()
+        check(lib.gpd_decode_tpv3(self.ctx().h, C.byref(ring.c), ring.offset % ring.num_blocks,
+                                  ring.num_blocks if max_blocks is None else int(max_blocks),
+                                  int(bool(add_vlan_header)), int(max_n), C.byref(r),
+                                  C.byref(ci.c()), C.byref(n), C.byref(nb), int(nthreads)),
+              "gpd_decode_tpv3")
+        k = n.value
+        out = BatchResult(res.status[:k], res.layers[:k], res.net_hash[:k], res.tp_hash[:k],
+                          res.csum[:k], None, res.hdr_off[:k])
+        return out, ci.head(k), nb.value
+
     def DecodeLayers(self, data: bytes, decoded: list):
         """parser.go:302-316 for one packet: fills `decoded`, sets self.Truncated, returns the
         error value (None on success)."""

@@ -264,3 +264,82 @@ def make_mixed(n: int, seed: int = 0x5EED0005) -> PacketBatch:
         b = parts[k % 3]
         pkts.append(b.packet(k // 3))
     return PacketBatch.from_packets(pkts)
+
+
+# ---- TPACKET_V3 rings (linux/if_packet.h layouts) for the AF_PACKET ingest -------------
+TPV3_BLOCK_DESC = 48      # sizeof(struct tpacket_block_desc)
+TPV3_HDR = 48             # sizeof(struct tpacket3_hdr)
+TPV3_HDRLEN = 48 + 20     # TPACKET_ALIGN(sizeof(tpacket3_hdr)) + sizeof(struct sockaddr_ll)
+TP_STATUS_USER, TP_STATUS_VLAN_VALID = 1, 16
+
+
+def _align16(x: int) -> int:
+    return (x + 15) & ~15
+
+
+def make_tpv3_ring(packets, block_size: int = 1 << 16, num_blocks: int = 8, first_block: int = 0,
+                   vlan=None, next_offset_zero_every: int = 3, ifindex: int = 7, seed: int = 0x5EED0006,
+                   empty_blocks=(), kernel_blocks=(), wire_extra: int = 0):
+    """A TPACKET_V3 ring as the kernel fills it (net/packet/af_packet.c layout): packets are
+    placed block by block from `first_block` on (wrapping); each frame sits at the kernel's
+    tp_mac (TPACKET_ALIGN(TPACKET3_HDRLEN + 16) - 14 for Ethernet); every
+    `next_offset_zero_every`-th packet leaves tp_next_offset 0 (the reader then steps by
+    tpAlign(snaplen + mac), afpacket/header.go:181-195).  `vlan`: per-packet (tci, valid) or
+    None.  Walk positions (0 = first_block) in `empty_blocks` are handed over with no
+    packets; those in `kernel_blocks`, and every block after the packets ran out, stay owned
+    by the kernel.
+    Returns (ring u8[num_blocks * block_size], blocks_used in ring order)."""
+    ring = np.zeros(num_blocks * block_size, np.uint8)
+    rng = np.random.default_rng(seed)
+    mac = _align16(TPV3_HDRLEN + 16) - 14
+    empty, kernel = set(empty_blocks), set(kernel_blocks)  # walk positions (0 = first_block)
+    k, used = 0, []
+    blk_i = 0
+    while k < len(packets) or any(e >= blk_i for e in empty):
+        if blk_i >= num_blocks:
+            raise ValueError("packets do not fit the ring")
+        b = (first_block + blk_i) % num_blocks
+        base = b * block_size
+        pos = _align16(TPV3_BLOCK_DESC)
+        first, n_in, prev = pos, 0, None
+        if blk_i not in empty:
+            while k < len(packets):
+                p = packets[k]
+                need = _align16(mac + len(p))
+                if pos + need > block_size:
+                    break
+                h = base + pos
+                sec, nsec = 1_700_000_000 + k, int(rng.integers(0, 10**9))
+                tci, valid = vlan[k] if vlan is not None else (0, False)
+                hdr = np.zeros(TPV3_HDR, np.uint8)
+                hdr[4:8] = np.frombuffer(np.uint32(sec).tobytes(), np.uint8)
+                hdr[8:12] = np.frombuffer(np.uint32(nsec).tobytes(), np.uint8)
+                hdr[12:16] = np.frombuffer(np.uint32(len(p)).tobytes(), np.uint8)
+                hdr[16:20] = np.frombuffer(np.uint32(len(p) + wire_extra).tobytes(), np.uint8)
+                st = TP_STATUS_USER | (TP_STATUS_VLAN_VALID if valid else 0)
+                hdr[20:24] = np.frombuffer(np.uint32(st).tobytes(), np.uint8)
+                hdr[24:26] = np.frombuffer(np.uint16(mac).tobytes(), np.uint8)
+                hdr[26:28] = np.frombuffer(np.uint16(mac + 14).tobytes(), np.uint8)
+                hdr[32:36] = np.frombuffer(np.uint32(tci).tobytes(), np.uint8)
+                ring[h:h + TPV3_HDR] = hdr
+                ring[h + 48 + 4:h + 48 + 8] = np.frombuffer(np.int32(ifindex).tobytes(), np.uint8)
+                ring[h + mac:h + mac + len(p)] = np.frombuffer(p, np.uint8)
+                if prev is not None:  # the previous packet's tp_next_offset
+                    nxt = 0 if (k - 1) % next_offset_zero_every == 0 else pos - prev
+                    ring[base + prev:base + prev + 4] = np.frombuffer(np.uint32(nxt).tobytes(), np.uint8)
+                prev = pos
+                pos += need
+                n_in += 1
+                k += 1
+        bd = np.zeros(TPV3_BLOCK_DESC, np.uint8)
+        bd[0:4] = np.frombuffer(np.uint32(3).tobytes(), np.uint8)  # TPACKET_V3
+        own = blk_i not in kernel
+        bd[8:12] = np.frombuffer(np.uint32(TP_STATUS_USER if own else 0).tobytes(), np.uint8)
+        bd[12:16] = np.frombuffer(np.uint32(n_in).tobytes(), np.uint8)
+        bd[16:20] = np.frombuffer(np.uint32(first).tobytes(), np.uint8)
+        bd[20:24] = np.frombuffer(np.uint32(pos).tobytes(), np.uint8)
+        bd[24:32] = np.frombuffer(np.uint64(blk_i + 1).tobytes(), np.uint8)
+        ring[base:base + TPV3_BLOCK_DESC] = bd
+        used.append(b)
+        blk_i += 1
+    return ring, used

@@ -12,7 +12,7 @@ import pytest
 
 from conftest import ROOT, gpu_available
 
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("gpd.h", "gpd_pcap.h", "gpd_flow.h")]
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("gpd.h", "gpd_pcap.h", "gpd_flow.h", "gpd_afpacket.h")]
 
 
 def declared_functions():
