@@ -34,6 +34,8 @@
 
 #include <cstdlib>
 
+#include <algorithm>
+
 #include "gpd_internal.h"
 
 namespace gpd {
@@ -1398,6 +1400,202 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void decode_kernel(KParams P) {
   }
 }
 
+// ---------------------------------------------------------------- register-staged fast loop
+typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+
+// LDS bytes per wave of rs_kernel: one window (the next one waits in VGPRs), plus the chunk
+// prefix sums of the cooperative checksum for windows of 8 KiB and more.
+__host__ __device__ constexpr uint32_t rs_wave_lds_bytes(int stage) {
+  return (uint32_t)stage + (stage >= 8192 ? (uint32_t)stage / 4u + 16u : 0u);
+}
+
+// The fast path's streaming loop with the window staged through registers: a window's bytes
+// are loaded with plain 16-byte-per-lane loads (nt: read once) into VGPRs while the previous
+// window is decoded out of the wave's single LDS buffer, then copied into that buffer with
+// ds_write_b128 at the top of the next iteration.  Descriptors are register loads two tiles
+// ahead.  Every load is compiler-visible, so each wait is the compiler's, placed at the first
+// use.  Measured on this part (tools/micro/hbm_mix.hip): the decode kernel's 72-B-read /
+// 32-B-write traffic shape streams at ~6.0 TB/s through registers against ~5.2 TB/s through
+// LDS-DMA, and one LDS buffer per wave (instead of two) frees LDS for more waves.
+// Iteration k:  commit window k (VGPR -> LDS)  ->  store the results of the tile the previous
+// window finished (deferred one iteration, so that after the next window's loads nothing else
+// is issued and the wait at the next commit covers exactly those loads)  ->  plan and load
+// window k+1  ->  decode window k from LDS.
+template <int STAGE, bool CS, bool HASH, int MINW, bool DEFER = true>
+__global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
+  constexpr int WAVES = 4;
+  constexpr int NC = STAGE / 1024;              // 16-byte chunks per lane per window
+  constexpr bool COOP = STAGE >= 8192;          // long segments: wave-cooperative checksum
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  for (uint32_t k = threadIdx.x; k < P.image_words; k += 64 * WAVES)
+    reinterpret_cast<uint32_t *>(g_lds)[k] = P.image[k];
+  __syncthreads();
+  const uint32_t img = (P.image_words * 4u + 15u) & ~15u;
+  const uint32_t buf = img + wave * rs_wave_lds_bytes(STAGE);
+  const uint32_t pfx = buf + STAGE;
+  const uint32_t n = (uint32_t)P.n;
+  const uint32_t ntiles = (n + 63u) >> 6;
+  const uint32_t nwaves = gridDim.x * WAVES;
+  const uint32_t dlen = (uint32_t)P.data_len;
+  const uint32_t fits = (uint32_t)STAGE - 15u;
+  const uint32_t options = P.options & ~kDiagMask;
+  const FastCtx F{P.eth_mult, ((uint32_t)GPD_LT_PAYLOAD << 8) | (reinterpret_cast<const uint8_t *>(g_lds)[GPD_LT_PAYLOAD]),
+                  (options & GPD_OPT_IGNORE_UNSUPPORTED) ? GPD_ST_OK : GPD_ST_UNSUPPORTED};
+
+  uint32_t tp = blockIdx.x * WAVES + wave;  // the planner's tile
+  if (tp >= ntiles) return;
+  auto dload = [&](uint32_t u, uint32_t &o, uint32_t &c) {  // descriptors of tile u
+    const uint32_t i = u * 64u + lane;
+    o = c = 0;
+    if (u < ntiles && i < n) {
+      o = __builtin_nontemporal_load(P.offset + i);
+      c = __builtin_nontemporal_load(P.caplen + i);
+    }
+  };
+  auto dread = [&](uint32_t u, uint32_t o_raw, uint32_t c_raw, uint32_t &off, uint32_t &end) -> uint32_t {
+    const uint32_t v = u * 64u + lane < n ? 1u : 0u;
+    const uint32_t o = v ? min(o_raw, dlen) : 0u;
+    const uint32_t l = v ? min(c_raw, dlen - o) : 0u;
+    off = o;  // a packet reaching past data_len is clamped to the buffer
+    end = o + l;
+    return v;
+  };
+  auto covered = [&](const Window &w, uint32_t pend, uint32_t off, uint32_t end) -> uint32_t {
+    return (pend && off >= w.base && end - w.base <= (uint32_t)STAGE) ? 1u : 0u;
+  };
+  // Window loads are unconditional (a chunk past the window's end re-reads its first 16
+  // bytes, a cached line), so every lane's registers come from this window's loads and the
+  // compiler needs no merge of older values: its only wait is at the commit.
+  v4u32 wv[NC];
+  auto wload = [&](const Window &w) {
+#pragma unroll
+    for (int j = 0; j < NC; j++) {
+      const uint32_t c = 1024u * j + 16u * lane;
+      wv[j] = __builtin_nontemporal_load(
+          reinterpret_cast<const v4u32 *>(P.data + w.base + (c < w.nbytes ? c : 0u)));
+    }
+    __builtin_amdgcn_sched_barrier(0);  // issue them here, ahead of the decode
+  };
+  auto wcommit = [&](const Window &) {
+#pragma unroll
+    for (int j = 0; j < NC; j++)
+      *reinterpret_cast<v4u32 *>(g_lds + buf + 1024u * j + 16u * lane) = wv[j];
+  };
+
+  // prologue: this tile's descriptors (waited for), the next two tiles' in flight
+  uint32_t o_a, c_a, o_b, c_b, off_p, end_p;
+  {
+    uint32_t o0, c0;
+    dload(tp, o0, c0);
+    dload(tp + nwaves, o_a, c_a);
+    dload(tp + 2u * nwaves, o_b, c_b);
+    (void)dread(tp, o0, c0, off_p, end_p);
+  }
+  uint32_t valid_p = tp * 64u + lane < n ? 1u : 0u;
+  uint32_t pend_p = (valid_p && end_p - off_p <= fits) ? 1u : 0u;
+  Window Wd = plan_window<STAGE>(pend_p != 0, off_p, end_p);
+  uint32_t cov_d = covered(Wd, pend_p, off_p, end_p);
+  pend_p &= cov_d ^ 1u;
+  wload(Wd);
+  uint32_t td = tp, off_d = off_p, end_d = end_p, valid_d = valid_p;
+  uint32_t big_d = valid_p & ((end_p - off_p <= fits) ? 0u : 1u);
+  bool first_d = true;
+  Out res{0, 0, 0, 0, 0, 0};
+  uint32_t fb = 0;
+  // results of a finished tile, stored one iteration later
+  bool st_pending = false;
+  uint32_t st_i = 0, st_valid = 0;
+  Out st_res{0, 0, 0, 0, 0, 0};
+  for (;;) {
+    // Wait order: every load issued in the previous iteration (descriptors two tiles ahead,
+    // then window k) is older than anything the wait below could over-cover, so the
+    // compiler's vmcnt at the first use of window k's registers costs nothing extra.
+    wcommit(Wd);  // window k: registers -> LDS (the compiler waits for its loads here)
+    // ---- plan the next window (the next tile's descriptors landed long ago)
+    Window Wn{0, 0};
+    uint32_t cov_n = 0;
+    bool has_next = false, new_tile = false;
+    if (__any(pend_p != 0)) {  // more of the planner's tile
+      has_next = true;
+    } else if (tp + nwaves < ntiles) {  // the next tile's first window
+      tp += nwaves;
+      valid_p = dread(tp, o_a, c_a, off_p, end_p);
+      o_a = o_b;
+      c_a = c_b;
+      pend_p = (valid_p && end_p - off_p <= fits) ? 1u : 0u;
+      has_next = new_tile = true;
+    }
+    // ---- the previous tile's results (a fallback lane's entry is rewritten later), issued
+    // before the next loads so that nothing follows those loads until their wait
+    if (DEFER && st_pending) {
+      if (st_valid) store_out(P, st_i, st_res);
+      st_pending = false;
+    }
+    if (new_tile) dload(tp + 2u * nwaves, o_b, c_b);
+    if (has_next) {
+      Wn = plan_window<STAGE>(pend_p != 0, off_p, end_p);
+      cov_n = covered(Wn, pend_p, off_p, end_p);
+      pend_p &= cov_n ^ 1u;
+      wload(Wn);
+    }
+    // ---- decode window k (tile td, the lanes it covers)
+    const uint32_t i = td * 64u + lane;
+    if (first_d && big_d) fb = 1;  // larger than a window: the generic decoder
+    Seg sg{0, 0, 0};
+    if (cov_d && (P.options & kDiagSkipDecode)) {  // diagnostics: data movement only
+      res = Out{g_lds[buf + ((off_d - Wd.base) & ~15u)], 0, 0, 0, 0, 0};
+    } else if (cov_d) {
+      if (!fast_decode<CS, HASH, COOP>(buf + (off_d - Wd.base), end_d - off_d, F, res, buf, sg)) fb = 1;
+    }
+    if constexpr (COOP) {  // long segments of this window: chunk prefix sums, shared
+      if (__any(sg.b > sg.a)) {
+        window_prefix<STAGE>(buf, pfx, lane);
+        if (sg.b > sg.a) {
+          const uint32_t mid = lds_u32(pfx + 4u * sg.b) - lds_u32(pfx + 4u * sg.a);
+          res.csum |= fold_le_not(sg.part + mid) << 16;
+        }
+      }
+    }
+    // ---- the tile is complete when the next window belongs to another tile (or none)
+    if (!has_next || new_tile) {
+      const uint64_t m = __ballot(fb != 0);  // the tile's leftovers go to the fallback list
+      if (m) {
+        uint32_t base = 0;
+        if (lane == (uint32_t)__builtin_ctzll(m)) base = atomicAdd(P.fb_count, (uint32_t)__popcll(m));
+        base = __builtin_amdgcn_readlane(base, (int)__builtin_ctzll(m));
+        if (fb) P.fb_list[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                      __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = i;
+      }
+      fb = 0;
+      if (DEFER) {
+        st_pending = true;
+        st_i = i;
+        st_valid = valid_d;
+        st_res = res;
+      } else if (valid_d) {
+        store_out(P, i, res);
+      }
+    }
+    if (!has_next) {
+      if (DEFER && st_valid) store_out(P, st_i, st_res);
+      break;
+    }
+    if (new_tile) {
+      td = tp;
+      off_d = off_p;
+      end_d = end_p;
+      valid_d = valid_p;
+      big_d = (valid_p && end_p - off_p > fits) ? 1u : 0u;
+      first_d = true;
+    } else {
+      first_d = false;
+    }
+    Wd = Wn;
+    cov_d = cov_n;
+  }
+}
+
 // The fallback list of the fast kernel: one lane per listed packet, bytes straight from
 // global memory (these packets are rare outside crafted inputs).
 template <bool PAGES>
@@ -1447,15 +1645,51 @@ static int geom() {
   return g;
 }
 
+template <int STAGE, bool CS, bool HASH, int MINW, bool DEFER = true>
+static hipError_t launch_rs(const KParams &P, hipStream_t stream, int num_cus) {
+  const uint64_t ntiles = (P.n + 63) / 64;
+  const size_t lds = ((P.image_words * 4u + 15u) & ~15u) + 4 * (size_t)rs_wave_lds_bytes(STAGE) + 64;
+  const uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>((160u * 1024u) / lds, MINW));
+  uint64_t blocks = (ntiles + 3) / 4;
+  const uint64_t cap = (uint64_t)num_cus * per_cu * 4;  // four rounds of resident workgroups
+  if (blocks > cap) blocks = cap;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL((rs_kernel<STAGE, CS, HASH, MINW, DEFER>), dim3((unsigned)blocks), dim3(256), lds, stream, P);
+  return hipGetLastError();
+}
+
+// Diagnostic selector GPD_RS_MINW (A/B only): waves per SIMD the register-staged kernel is
+// compiled for.
+static int rs_minw() {
+  static int w = -1;
+  if (w < 0) {
+    const char *e = getenv("GPD_RS_MINW");
+    w = e ? atoi(e) : 0;
+  }
+  return w;
+}
+
 // the fast kernel reads headers at any byte address: linear windows
 template <bool CS, bool HASH>
 static hipError_t launch_fast(const KParams &P, hipStream_t stream, int num_cus) {
-  // Register budgets match what LDS admits: 4 KiB windows fit four 4-wave workgroups per CU
-  // (4 waves per SIMD, <= 128 VGPRs each), 8 KiB windows two (2 waves per SIMD).  Without
-  // the bound the compiler may cross 128 VGPRs and silently drop a wave per SIMD.
-  if (P.stage == 4096)
-    return launch_t<4096, true, false, false, false, 4, CS, HASH, 4>(P, stream, num_cus);
-  return launch_t<8192, true, false, false, false, 4, CS, HASH, 2>(P, stream, num_cus);
+  if (geom() == 3) {  // A/B: the LDS-DMA double-buffered loop
+    // Register budgets match what LDS admits: 4 KiB windows fit four 4-wave workgroups per
+    // CU (4 waves per SIMD, <= 128 VGPRs each), 8 KiB windows two (2 waves per SIMD).
+    if (P.stage == 4096)
+      return launch_t<4096, true, false, false, false, 4, CS, HASH, 4>(P, stream, num_cus);
+    return launch_t<8192, true, false, false, false, 4, CS, HASH, 2>(P, stream, num_cus);
+  }
+  // register-staged loop; the register bound sets the waves per SIMD (VGPRs <= 512 / MINW)
+  // (defaults: 3 waves per SIMD for 4 KiB windows, 2 for 8 KiB: the most without spills)
+  const int w = rs_minw();
+  if (P.stage == 4096) {
+    if (w == 2) return launch_rs<4096, CS, HASH, 2>(P, stream, num_cus);
+    if (w == 4) return launch_rs<4096, CS, HASH, 4>(P, stream, num_cus);  // A/B (spills)
+    if (w == 5) return launch_rs<4096, CS, HASH, 4, false>(P, stream, num_cus);  // A/B
+    if (w == 6) return launch_rs<4096, CS, HASH, 3, false>(P, stream, num_cus);  // A/B
+    return launch_rs<4096, CS, HASH, 3>(P, stream, num_cus);
+  }
+  return launch_rs<8192, CS, HASH, 2>(P, stream, num_cus);
 }
 
 template <bool EXT, bool PAGES>

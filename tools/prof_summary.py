@@ -25,7 +25,7 @@ def counters(d, name):
     meta = {}
     for f in glob.glob(os.path.join(d, name, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "decode_kernel" in r["Kernel_Name"]:
+            if "decode_kernel" in r["Kernel_Name"] or "rs_kernel" in r["Kernel_Name"]:
                 acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
                 meta = {k: r[k] for k in ("Kernel_Name", "Grid_Size", "Workgroup_Size",
                                           "LDS_Block_Size", "VGPR_Count", "SGPR_Count",
