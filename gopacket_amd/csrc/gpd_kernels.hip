@@ -640,13 +640,7 @@ __device__ __forceinline__ uint32_t dot2(uint32_t x, uint32_t w, uint32_t acc) {
 struct __attribute__((packed, aligned(1))) U128 {
   uint32_t x, y, z, w;
 };
-struct __attribute__((packed, aligned(1))) U64 {
-  uint32_t x, y;
-};
-typedef uint32_t __attribute__((aligned(1))) U32;
 __device__ __forceinline__ U128 ld128(uint32_t a) { return *reinterpret_cast<const U128 *>(g_lds + a); }
-__device__ __forceinline__ U64 ld64(uint32_t a) { return *reinterpret_cast<const U64 *>(g_lds + a); }
-__device__ __forceinline__ uint32_t ld32(uint32_t a) { return *reinterpret_cast<const U32 *>(g_lds + a); }
 
 // big-endian 16-bit value of bytes (0,1) / (2,3) of a little-endian word
 __device__ __forceinline__ uint32_t be_lo(uint32_t w) { return __builtin_amdgcn_perm(0u, w, 0x0C0C0001u); }
@@ -661,31 +655,6 @@ __device__ __forceinline__ uint32_t fold_le_not(uint32_t s) {
   s = (s >> 16) + (s & 0xFFFFu);
   s = (s >> 16) + (s & 0xFFFFu);
   return __builtin_amdgcn_perm(0u, ~s, 0x0C0C0001u);  // byte-swap the low half, high half 0
-}
-
-// LE-domain sum of the 16-bit halves of the L bytes at LDS address p (an odd last byte
-// counts as the low byte of its half, i.e. << 8 in the big-endian domain).
-__device__ __forceinline__ uint32_t lesum_lds(uint32_t p, uint32_t L, uint32_t acc) {
-  uint32_t x = 0;
-  for (; x + 16u <= L; x += 16u) {
-    const U128 q = ld128(p + x);
-    acc = dot2(q.x, 0x00010001u, acc);
-    acc = dot2(q.y, 0x00010001u, acc);
-    acc = dot2(q.z, 0x00010001u, acc);
-    acc = dot2(q.w, 0x00010001u, acc);
-  }
-  if (x < L) {  // 1..15 ragged bytes: keep the first r of the next 16
-    const U128 q = ld128(p + x);
-    const uint32_t r8 = (L - x) * 8u;
-    uint64_t lo = ((uint64_t)q.y << 32) | q.x, hi = ((uint64_t)q.w << 32) | q.z;
-    lo = r8 >= 64u ? lo : (lo << (64u - r8)) >> (64u - r8);
-    hi = r8 > 64u ? (hi << (128u - r8)) >> (128u - r8) : 0ull;
-    acc = dot2((uint32_t)lo, 0x00010001u, acc);
-    acc = dot2((uint32_t)(lo >> 32), 0x00010001u, acc);
-    acc = dot2((uint32_t)hi, 0x00010001u, acc);
-    acc = dot2((uint32_t)(hi >> 32), 0x00010001u, acc);
-  }
-  return acc;
 }
 
 // FNV-1a (flows.go:60-67) on (lo, hi) halves.  h * fnvPrime with fnvPrime = 2^40 + 0x1b3:
@@ -759,9 +728,13 @@ __device__ __forceinline__ uint32_t tag_type(uint32_t et) {
   return (et == 0x8100u || et == 0x88A8u) ? 1u : 0u;
 }
 
-__device__ __forceinline__ void load80(uint32_t (&W)[20], uint32_t a) {
+// The 64 bytes from a network header on (it and the first 16 bytes after it need <= 56),
+// as four ds_read_b128 at the header's own byte address.  Misaligned, each costs ~3.6x an
+// aligned one on gfx950, but aligned dword reads of the same bytes are slower still when
+// packets sit at power-of-two strides (bank conflicts: tools/micro/lds_align.hip).
+__device__ __forceinline__ void load64(uint32_t (&W)[16], uint32_t a) {
 #pragma unroll
-  for (int k = 0; k < 5; k++) {
+  for (int k = 0; k < 4; k++) {
     const U128 q = ld128(a + 16 * k);
     W[4 * k] = q.x; W[4 * k + 1] = q.y; W[4 * k + 2] = q.z; W[4 * k + 3] = q.w;
   }
@@ -816,12 +789,13 @@ __device__ __forceinline__ void window_prefix(uint32_t buf, uint32_t pfx, uint32
 // p: LDS address of the packet's first byte; len: its length.  CS / HASH: the fused
 // checksums / flow hashes are requested (GPD_OPT_NO_CHECKSUMS / _NO_FLOW_HASH clear).
 // Two dependent LDS round trips per pass (three for tagged frames): (1) the Ethernet header
-// and the 80 bytes after it; (2) every table lookup — EtherType, protocol, ports, each on
+// and the 64 bytes after it; (2) every table lookup — EtherType, protocol, ports, each on
 // a guess read from the bytes (IPv4/IPv6 by the version nibble, TCP/UDP by the protocol
-// number) — together with the transport segment's first and last 16-byte chunks.  The
-// lookups then confirm the guesses; a packet they contradict goes to the generic decoder.
-// Hashes and checksums are computed from registers as each layer is accepted, so VXLAN's
-// second pass overwrites them exactly as the reused layer objects are overwritten (A11).
+// number).  The lookups then confirm the guesses; a packet they contradict goes to the
+// generic decoder.  Hashes and the IPv4 header checksum are computed from registers as
+// each layer is accepted, so VXLAN's second pass overwrites them exactly as the reused
+// layer objects are overwritten (A11); the transport checksum reads its segment's edge
+// chunks once more after the parse.
 // COOP: a long even-aligned segment's whole middle chunks are left to window_prefix (sg).
 template <bool CS, bool HASH, bool COOP>
 __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const FastCtx &F, Out &o,
@@ -832,20 +806,19 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
   uint32_t tp_off = 0, tp_len = 0, tp_pl = 0;  // the last transport; its proto + length terms
   uint32_t tp_kind = 0, ps4 = 0, ps6 = 0;      // its network object kind; each kind's addresses
   uint32_t net_off = 0;                        // the last network header
-  U128 c0{0, 0, 0, 0}, ct{0, 0, 0, 0};        // its segment's first / ragged-last chunk
   uint32_t b = 0, lim = len;                   // this pass's Ethernet offset; end of its data
   auto put = [&](uint32_t code) { codes |= (uint64_t)code << (16 + 4 * nc); nc++; };
   for (int pass = 0; pass < 2; pass++) {
     // ---- round trip 1: Ethernet header (ethernet.go:41-62) and the bytes after it
     if (lim < b + 15u) return false;  // too small, or an empty payload: generic path
     const U128 e = ld128(p + b + 8);  // bytes 8..23: EtherType and up to two tags
-    uint32_t W[20];
-    load80(W, p + b + 14);
+    uint32_t W[16];
+    load64(W, p + b + 14);
     const uint32_t et0 = be_lo(e.y), et1 = be_lo(e.z), et2 = be_lo(e.w);
     if (et0 < 0x0600u) return false;  // 802.3 length framing
     const uint32_t t1 = tag_type(et0), t2 = t1 & tag_type(et1);
     const uint32_t l3 = b + 14 + 4 * (t1 + t2);
-    if (t1) load80(W, p + l3);  // tagged: the network header is further in
+    if (t1) load64(W, p + l3);  // tagged: the network header is further in
     // ---- guesses from the bytes
     const uint32_t ver = (W[0] >> 4) & 15u;
     const bool v4 = ver == 4u;
@@ -860,8 +833,7 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
     else plen = (length > dl - 40u) ? dl - 40u : length;
     const uint32_t ulen = be_lo(ty);
     const uint32_t seg = (g == 2u && ulen >= 8u && ulen <= plen) ? ulen : plen;
-    const uint32_t xt = (seg < 16384u ? seg : 0u) & ~15u;  // (a guess: keep it in the window)
-    // ---- round trip 2: all lookups, and the segment chunks
+    // ---- round trip 2: all lookups
     const uint32_t r0 = fix_bucket<kFixEthBase>(F.mult, et0);
     uint32_t r1 = 0, r2 = 0;
     if (t1) {
@@ -872,7 +844,6 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
     const uint32_t pbase = g == 1u ? kFixTcpBase : kFixUdpBase;
     const uint32_t rd = fix_bucket_at(pbase, F.mult, be_hi(tx));
     const uint32_t rs = fix_bucket_at(pbase, F.mult, be_lo(tx));
-    const U128 n0 = ld128(p + l4), nt = ld128(p + l4 + xt);
     // ---- Ethernet / Dot1Q (dot1q.go:29-50), confirming the tag guesses
     put(GPD_C_ETHERNET);
     if (((r0 & 15u) == D_DOT1Q) != (t1 != 0)) return false;
@@ -966,8 +937,6 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
     tp_kind = net;
     tp_off = l4;
     tp_len = seg;
-    c0 = n0;
-    ct = nt;
     const uint32_t pl4 = seg - hl;
     if (pl4 == 0) break;
     const uint32_t next = ports_next_raw(rd, rs, F.pl_raw), nd = next & 15u;
@@ -1021,7 +990,10 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
     return true;
   }
   if (CS) {
-    // TCP.ComputeChecksum(), tcp.go:193-195 / tcpip.go:52-88 over the last transport
+    // TCP.ComputeChecksum(), tcp.go:193-195 / tcpip.go:52-88 over the last transport.  Its
+    // first and ragged-last 16-byte chunks are read here, once, after the parse (holding
+    // them through the parse would cost 16 VGPRs, a wave per SIMD).
+    const U128 c0 = ld128(p + tp_off), ct = ld128(p + tp_off + (tp_len & ~15u));
     uint32_t s = tp_ps;
     const uint32_t w0 = tp_len >= 16u ? 0x00010001u : 0u;  // first whole chunk
     s = dot2(c0.x, w0, s);
@@ -1421,7 +1393,7 @@ __host__ __device__ constexpr uint32_t rs_wave_lds_bytes(int stage) {
 // window finished (deferred one iteration, so that after the next window's loads nothing else
 // is issued and the wait at the next commit covers exactly those loads)  ->  plan and load
 // window k+1  ->  decode window k from LDS.
-template <int STAGE, bool CS, bool HASH, int MINW, bool DEFER = true>
+template <int STAGE, bool CS, bool HASH, int MINW, bool DEFER = false>
 __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
   constexpr int WAVES = 4;
   constexpr int NC = STAGE / 1024;              // 16-byte chunks per lane per window
@@ -1645,7 +1617,7 @@ static int geom() {
   return g;
 }
 
-template <int STAGE, bool CS, bool HASH, int MINW, bool DEFER = true>
+template <int STAGE, bool CS, bool HASH, int MINW, bool DEFER = false>
 static hipError_t launch_rs(const KParams &P, hipStream_t stream, int num_cus) {
   const uint64_t ntiles = (P.n + 63) / 64;
   const size_t lds = ((P.image_words * 4u + 15u) & ~15u) + 4 * (size_t)rs_wave_lds_bytes(STAGE) + 64;
@@ -1680,16 +1652,16 @@ static hipError_t launch_fast(const KParams &P, hipStream_t stream, int num_cus)
     return launch_t<8192, true, false, false, false, 4, CS, HASH, 2>(P, stream, num_cus);
   }
   // register-staged loop; the register bound sets the waves per SIMD (VGPRs <= 512 / MINW)
-  // (defaults: 3 waves per SIMD for 4 KiB windows, 2 for 8 KiB: the most without spills)
+  // (defaults: 4 waves per SIMD for 4 KiB windows, 3 for 8 KiB: what LDS admits, no spills)
   const int w = rs_minw();
   if (P.stage == 4096) {
     if (w == 2) return launch_rs<4096, CS, HASH, 2>(P, stream, num_cus);
-    if (w == 4) return launch_rs<4096, CS, HASH, 4>(P, stream, num_cus);  // A/B (spills)
-    if (w == 5) return launch_rs<4096, CS, HASH, 4, false>(P, stream, num_cus);  // A/B
-    if (w == 6) return launch_rs<4096, CS, HASH, 3, false>(P, stream, num_cus);  // A/B
-    return launch_rs<4096, CS, HASH, 3>(P, stream, num_cus);
+    if (w == 3) return launch_rs<4096, CS, HASH, 3>(P, stream, num_cus);
+    if (w == 6) return launch_rs<4096, CS, HASH, 3, true>(P, stream, num_cus);  // A/B
+    return launch_rs<4096, CS, HASH, 4>(P, stream, num_cus);
   }
-  return launch_rs<8192, CS, HASH, 2>(P, stream, num_cus);
+  if (w == 2) return launch_rs<8192, CS, HASH, 2>(P, stream, num_cus);
+  return launch_rs<8192, CS, HASH, 3>(P, stream, num_cus);
 }
 
 template <bool EXT, bool PAGES>
