@@ -1440,12 +1440,13 @@ __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
   // bytes, a cached line), so every lane's registers come from this window's loads and the
   // compiler needs no merge of older values: its only wait is at the commit.
   v4u32 wv[NC];
+  const bool ntl = (P.options & kDiagNtLoad) != 0;  // read-once policy (default on; A/B knob)
   auto wload = [&](const Window &w) {
 #pragma unroll
     for (int j = 0; j < NC; j++) {
       const uint32_t c = 1024u * j + 16u * lane;
-      wv[j] = __builtin_nontemporal_load(
-          reinterpret_cast<const v4u32 *>(P.data + w.base + (c < w.nbytes ? c : 0u)));
+      const v4u32 *a = reinterpret_cast<const v4u32 *>(P.data + w.base + (c < w.nbytes ? c : 0u));
+      wv[j] = ntl ? __builtin_nontemporal_load(a) : *a;
     }
     __builtin_amdgcn_sched_barrier(0);  // issue them here, ahead of the decode
   };
@@ -1479,11 +1480,14 @@ __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
   bool st_pending = false;
   uint32_t st_i = 0, st_valid = 0;
   Out st_res{0, 0, 0, 0, 0, 0};
+  PH_DECL
   for (;;) {
+    PH_MARK(5);  // loop overhead / tail of the previous iteration
     // Wait order: every load issued in the previous iteration (descriptors two tiles ahead,
     // then window k) is older than anything the wait below could over-cover, so the
     // compiler's vmcnt at the first use of window k's registers costs nothing extra.
     wcommit(Wd);  // window k: registers -> LDS (the compiler waits for its loads here)
+    PH_MARK(0);  // waiting for the window (and copying it)
     // ---- plan the next window (the next tile's descriptors landed long ago)
     Window Wn{0, 0};
     uint32_t cov_n = 0;
@@ -1511,6 +1515,7 @@ __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
       pend_p &= cov_n ^ 1u;
       wload(Wn);
     }
+    PH_MARK(1);  // stores of the previous tile, planning and issuing the next window
     // ---- decode window k (tile td, the lanes it covers)
     const uint32_t i = td * 64u + lane;
     if (first_d && big_d) fb = 1;  // larger than a window: the generic decoder
@@ -1520,6 +1525,7 @@ __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
     } else if (cov_d) {
       if (!fast_decode<CS, HASH, COOP>(buf + (off_d - Wd.base), end_d - off_d, F, res, buf, sg)) fb = 1;
     }
+    PH_MARK(2);  // decode
     if constexpr (COOP) {  // long segments of this window: chunk prefix sums, shared
       if (__any(sg.b > sg.a)) {
         window_prefix<STAGE>(buf, pfx, lane);
@@ -1529,6 +1535,7 @@ __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
         }
       }
     }
+    PH_MARK(3);  // cooperative checksum
     // ---- the tile is complete when the next window belongs to another tile (or none)
     if (!has_next || new_tile) {
       const uint64_t m = __ballot(fb != 0);  // the tile's leftovers go to the fallback list
@@ -1549,8 +1556,10 @@ __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
         store_out(P, i, res);
       }
     }
+    PH_MARK(4);  // fallback list (and this tile's stores when not deferred)
     if (!has_next) {
       if (DEFER && st_valid) store_out(P, st_i, st_res);
+      PH_FLUSH;
       break;
     }
     if (new_tile) {
@@ -1623,7 +1632,8 @@ static hipError_t launch_rs(const KParams &P, hipStream_t stream, int num_cus) {
   const size_t lds = ((P.image_words * 4u + 15u) & ~15u) + 4 * (size_t)rs_wave_lds_bytes(STAGE) + 64;
   const uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>((160u * 1024u) / lds, MINW));
   uint64_t blocks = (ntiles + 3) / 4;
-  const uint64_t cap = (uint64_t)num_cus * per_cu * 4;  // four rounds of resident workgroups
+  static const int rounds = getenv("GPD_ROUNDS") ? atoi(getenv("GPD_ROUNDS")) : 4;  // A/B only
+  const uint64_t cap = (uint64_t)num_cus * per_cu * (rounds > 0 ? rounds : 4);  // rounds of resident workgroups
   if (blocks > cap) blocks = cap;
   if (blocks == 0) return hipSuccess;
   hipLaunchKernelGGL((rs_kernel<STAGE, CS, HASH, MINW, DEFER>), dim3((unsigned)blocks), dim3(256), lds, stream, P);
