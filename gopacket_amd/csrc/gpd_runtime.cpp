@@ -243,6 +243,27 @@ struct gpd_ctx {
   }
 };
 
+// Host-side copies of the staging pipeline run on up to 16 threads: fn(lo, hi) over [0, n).
+template <class F>
+static void par_for(uint64_t n, uint64_t grain, F fn) {
+  static const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  const uint64_t T = std::min<uint64_t>(hw, (n + grain - 1) / grain);
+  if (T <= 1) {
+    fn(0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (uint64_t t = 1; t < T; t++) th.emplace_back([&, t] { fn(n * t / T, n * (t + 1) / T); });
+  fn(0, n / T);
+  for (auto &x : th) x.join();
+}
+
+static void par_memcpy(void *dst, const void *src, uint64_t bytes) {
+  par_for(bytes, 4u << 20, [&](uint64_t lo, uint64_t hi) {
+    std::memcpy(static_cast<uint8_t *>(dst) + lo, static_cast<const uint8_t *>(src) + lo, hi - lo);
+  });
+}
+
 namespace gpd {
 int ctx_device(const gpd_ctx *ctx) { return ctx->device; }
 int ctx_num_cus(const gpd_ctx *ctx) { return ctx->num_cus; }
@@ -576,13 +597,16 @@ static int alloc_slots(gpd_ctx *ctx, uint64_t bytes, uint64_t pkts, bool ext) {
 
 static void drain_slot(gpd_ctx::Slot &s, const gpd_result *out) {
   const uint64_t m = s.hi - s.lo;
-  std::memcpy(out->status + s.lo, s.h_status, m * 4);
-  std::memcpy(out->layers + s.lo, s.h_layers, m * 8);
-  if (out->csum) std::memcpy(out->csum + s.lo, s.h_csum, m * 4);
-  if (out->net_hash) std::memcpy(out->net_hash + s.lo, s.h_nh, m * 8);
-  if (out->tp_hash) std::memcpy(out->tp_hash + s.lo, s.h_th, m * 8);
-  if (out->hdr_off) std::memcpy(out->hdr_off + s.lo, s.h_hoff, m * 4);
-  if (out->ext) std::memcpy(out->ext + s.lo, s.h_ext, m * sizeof(gpd_ext_rec));
+  par_for(m, 1u << 16, [&](uint64_t a, uint64_t b) {
+    const uint64_t c = b - a;
+    std::memcpy(out->status + s.lo + a, s.h_status + a, c * 4);
+    std::memcpy(out->layers + s.lo + a, s.h_layers + a, c * 8);
+    if (out->csum) std::memcpy(out->csum + s.lo + a, s.h_csum + a, c * 4);
+    if (out->net_hash) std::memcpy(out->net_hash + s.lo + a, s.h_nh + a, c * 8);
+    if (out->tp_hash) std::memcpy(out->tp_hash + s.lo + a, s.h_th + a, c * 8);
+    if (out->hdr_off) std::memcpy(out->hdr_off + s.lo + a, s.h_hoff + a, c * 4);
+    if (out->ext) std::memcpy(out->ext + s.lo + a, s.h_ext + a, c * sizeof(gpd_ext_rec));
+  });
   s.busy = false;
 }
 
@@ -603,28 +627,61 @@ int gpd_decode_host(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out) {
       HIP_TRY(hipStreamSynchronize(s.stream));
       drain_slot(s, out);
     }
-    // gather packets [i, j) whose bytes fit the slot, rebased to a 16-aligned start
+    // Span mode: packets [i, j) lie inside one window of the source buffer of at most kBytes
+    // with few gaps (the usual back-to-back batch): that window travels as it is (straight
+    // from the caller's buffer when it is registered) and the offsets are rebased.
+    // Otherwise the packets are repacked 16-byte aligned into the slot.
     uint64_t j = i, used = 0;
+    const uint64_t lo16 = std::min<uint64_t>(in->offset[i], in->data_len) & ~15ull;
+    uint64_t span_hi = lo16;
     while (j < in->n && j - i < kPkts) {
-      const uint32_t len = in->caplen[j];
-      const uint64_t need = ((used + 15) & ~15ull) + len;
-      if (need > kBytes) break;
-      used = need;
+      const uint64_t o = in->offset[j], e = o + in->caplen[j];
+      if (o < lo16 || e > in->data_len || e - lo16 > kBytes) break;
+      span_hi = std::max(span_hi, e);
+      used += in->caplen[j];
       j++;
     }
-    if (j == i) return set_err(GPD_ERR_INVALID, "gpd_decode_host: packet %llu larger than %llu bytes",
-                               (unsigned long long)i, (unsigned long long)kBytes);
+    const bool span = j > i && (span_hi - lo16) <= 2 * used + 4096;
     uint64_t pos = 0;
-    for (uint64_t p = i; p < j; p++) {
-      pos = (pos + 15) & ~15ull;
-      const uint32_t len = in->caplen[p];
-      std::memcpy(s.h_data + pos, in->data + in->offset[p], len);
-      s.h_off[p - i] = (uint32_t)pos;
-      s.h_len[p - i] = len;
-      pos += len;
+    if (span) {
+      pos = span_hi - lo16;
+      const uint64_t m = j - i;
+      par_for(m, 1u << 16, [&](uint64_t a, uint64_t b) {
+        for (uint64_t p = a; p < b; p++) s.h_off[p] = (uint32_t)(in->offset[i + p] - lo16);
+        std::memcpy(s.h_len + a, in->caplen + i + a, (b - a) * 4);
+      });
+      const uint64_t bytes = std::min<uint64_t>((pos + 15) & ~15ull, ((in->data_len + 15) & ~15ull) - lo16);
+      if (ctx->is_registered(in->data + lo16, bytes)) {
+        HIP_TRY(hipMemcpyAsync(s.d_data, in->data + lo16, bytes, hipMemcpyHostToDevice, s.stream));
+      } else {
+        par_memcpy(s.h_data, in->data + lo16, bytes);
+        HIP_TRY(hipMemcpyAsync(s.d_data, s.h_data, bytes, hipMemcpyHostToDevice, s.stream));
+      }
+    } else {
+      j = i;
+      used = 0;
+      while (j < in->n && j - i < kPkts) {
+        const uint32_t len = in->caplen[j];
+        const uint64_t need = ((used + 15) & ~15ull) + len;
+        if (need > kBytes) break;
+        used = need;
+        j++;
+      }
+      if (j == i) return set_err(GPD_ERR_INVALID, "gpd_decode_host: packet %llu larger than %llu bytes",
+                                 (unsigned long long)i, (unsigned long long)kBytes);
+      for (uint64_t p = i; p < j; p++) {  // positions (cheap), then the copies in parallel
+        pos = (pos + 15) & ~15ull;
+        s.h_off[p - i] = (uint32_t)pos;
+        s.h_len[p - i] = in->caplen[p];
+        pos += in->caplen[p];
+      }
+      par_for(j - i, 1u << 14, [&](uint64_t a, uint64_t b) {
+        for (uint64_t p = a; p < b; p++)
+          std::memcpy(s.h_data + s.h_off[p], in->data + in->offset[i + p], s.h_len[p]);
+      });
+      HIP_TRY(hipMemcpyAsync(s.d_data, s.h_data, (pos + 15) & ~15ull, hipMemcpyHostToDevice, s.stream));
     }
     const uint64_t m = j - i;
-    HIP_TRY(hipMemcpyAsync(s.d_data, s.h_data, (pos + 15) & ~15ull, hipMemcpyHostToDevice, s.stream));
     HIP_TRY(hipMemcpyAsync(s.d_off, s.h_off, m * 4, hipMemcpyHostToDevice, s.stream));
     HIP_TRY(hipMemcpyAsync(s.d_len, s.h_len, m * 4, hipMemcpyHostToDevice, s.stream));
     gpd_batch b{s.d_data, pos, s.d_off, s.d_len, m};

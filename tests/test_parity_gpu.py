@@ -188,13 +188,28 @@ def test_options_no_checksums_no_hashes():
 
 
 def test_host_path_matches_device_path():
+    """gpd_decode_host in both staging modes: span (a back-to-back batch travels as one
+    window of the caller's buffer) and repack (shuffled / overlapping / gappy layouts), with
+    and without the buffer registered, against the device path."""
     from gopacket_amd import parser as P
+    from gopacket_amd._lib import check, lib
     b = synth.make_mixed(5000)
     p = P.DecodingLayerParser(L.LayerTypeEthernet)
     p._mask = ALL
     dev = p.DecodeBatch(b, ext=True)
     host = p.DecodeBatchHost(b, ext=True)
     assert_same(host, dev, b)
+    check(lib.gpd_host_register(p.ctx().h, b.data.ctypes.data, b.data.nbytes), "gpd_host_register")
+    try:
+        assert_same(p.DecodeBatchHost(b, ext=True), dev, b)
+    finally:
+        lib.gpd_host_unregister(p.ctx().h, b.data.ctypes.data)
+    rng = np.random.default_rng(2)
+    perm = rng.permutation(b.n)
+    shuffled = PacketBatch(b.data, b.data_len, b.offset[perm].copy(), b.caplen[perm].copy())
+    assert_same(p.DecodeBatchHost(shuffled, ext=True), p.DecodeBatch(shuffled, ext=True), shuffled)
+    sparse = PacketBatch(b.data, b.data_len, b.offset[::7].copy(), b.caplen[::7].copy())  # gaps
+    assert_same(p.DecodeBatchHost(sparse, ext=False), p.DecodeBatch(sparse, ext=False), sparse, ext=False)
 
 
 def test_decode_layers_single_packet_api():
