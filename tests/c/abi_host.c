@@ -9,9 +9,16 @@
  * u32 caplen[n].  The batch is decoded three ways and every output word is compared:
  *   1. gpd_decode on device buffers (hipMalloc + hipMemcpy, the caller's own stream),
  *   2. gpd_decode_host (host arrays, pinned double-buffered staging inside the library),
- *   3. the CPU oracle (oracle/libgpd_oracle.so, test infrastructure) as the checker.
- * Prints "abi_host ok N" and exits 0 when all three agree bit for bit.
+ *   3. the CPU oracle (oracle/libgpd_oracle.so, test infrastructure) as the checker,
+ *   4. gpd_decode_pcap over an in-memory pcap file holding the same packets (records at
+ *      unaligned offsets, raw capture bytes sent to HBM),
+ * and then the device results feed the flow table (gpd_flow_insert on the caller's stream):
+ * every packet's flow record must hold exactly the key bytes at the packet's hdr_off
+ * positions, the per-record packet/byte/first/last counters must match a recount, records
+ * must have pairwise distinct keys, and gpd_flow_stats must add up.
+ * Prints "abi_host ok N F" (F = flows) and exits 0 when everything agrees bit for bit.
  */
+#include <stddef.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -20,6 +27,8 @@
 #include <hip/hip_runtime_api.h>
 
 #include "../../include/gpd.h"
+#include "../../include/gpd_flow.h"
+#include "../../include/gpd_pcap.h"
 #include "../../oracle/gpd_oracle.h"
 
 #define CHECK(x)                                                                    \
@@ -73,6 +82,111 @@ static int res_cmp(const char *what, const res_t *a, const res_t *b, uint64_t n)
     }
   }
   return 0;
+}
+
+/* Key of packet i as the flow table stores it (gpd_flow.h): network endpoints at the
+ * network-layer offset, ports at the transport offset. */
+static int key_matches(const gpd_flow_rec *r, const uint8_t *pkt, uint32_t hoff) {
+  const uint32_t no = GPD_HDR_NET(hoff), to = GPD_HDR_TP(hoff);
+  if (no == GPD_HDR_NONE || to == GPD_HDR_NONE) return 0;
+  const uint8_t *src = r->addr_len == 4 ? pkt + no + 12 : pkt + no + 8;
+  const uint8_t *dst = src + r->addr_len;
+  return memcmp(r->src, src, r->addr_len) == 0 && memcmp(r->dst, dst, r->addr_len) == 0 &&
+         memcmp(r->sport, pkt + to, 2) == 0 && memcmp(r->dport, pkt + to + 2, 2) == 0;
+}
+
+static int rec_key_cmp(const void *a, const void *b) {
+  const gpd_flow_rec *x = a, *y = b;
+  /* compare every key field: types, length, addresses, ports (fields are contiguous) */
+  return memcmp(x->src, y->src, offsetof(gpd_flow_rec, reserved) - offsetof(gpd_flow_rec, src));
+}
+
+static int check_flows(gpd_ctx *ctx, hipStream_t s, const gpd_batch *db, const gpd_result *dr,
+                       const uint8_t *data, const uint32_t *off, const uint32_t *cap,
+                       const uint32_t *hdr_off, uint64_t n, uint64_t *flows_out) {
+  gpd_flowtable *ft = NULL;
+  CHECK(gpd_flow_create(ctx, 2 * n + 64, &ft));
+  uint32_t *d_id, *id = malloc(4 * n + 4);
+  HCHECK(hipMalloc((void **)&d_id, 4 * n + 4));
+  CHECK(gpd_flow_insert(ft, db, dr, d_id, 1000, s));
+  gpd_flow_stats st;
+  CHECK(gpd_flow_stats_get(ft, &st, s));
+  HCHECK(hipMemcpy(id, d_id, 4 * n, hipMemcpyDeviceToHost));
+  gpd_flow_rec *rec = calloc(st.flows + 1, sizeof *rec);
+  uint32_t *ridx = calloc(st.flows + 1, 4);
+  uint64_t nrec = 0;
+  CHECK(gpd_flow_export(ft, rec, ridx, st.flows, &nrec, s));
+  int bad = nrec != st.flows || st.full != 0 || st.collisions != 0;
+  /* record index -> export slot */
+  uint64_t *pk = calloc(nrec + 1, 8), *by = calloc(nrec + 1, 8), *lo = calloc(nrec + 1, 8),
+           *hi = calloc(nrec + 1, 8);
+  uint64_t assigned = 0, none = 0;
+  for (uint64_t i = 0; i < n && !bad; i++) {
+    if (id[i] == GPD_FLOW_NONE) {
+      none++;
+      continue;
+    }
+    uint64_t k = 0;
+    while (k < nrec && ridx[k] != id[i]) k++;
+    if (k == nrec || !key_matches(&rec[k], data + off[i], hdr_off[i])) {
+      fprintf(stderr, "flow: packet %llu id %u has no matching record\n", (unsigned long long)i, id[i]);
+      bad = 1;
+      break;
+    }
+    const uint64_t seq = 1000 + i;
+    if (pk[k] == 0 || seq < lo[k]) lo[k] = seq;
+    if (pk[k] == 0 || seq > hi[k]) hi[k] = seq;
+    pk[k]++;
+    by[k] += cap[i];
+    assigned++;
+  }
+  for (uint64_t k = 0; k < nrec && !bad; k++)
+    if (rec[k].packets != pk[k] || rec[k].bytes != by[k] || rec[k].first != lo[k] ||
+        rec[k].last != hi[k]) {
+      fprintf(stderr, "flow: record %u counters differ\n", ridx[k]);
+      bad = 1;
+    }
+  if (!bad) {
+    qsort(rec, nrec, sizeof *rec, rec_key_cmp);
+    for (uint64_t k = 1; k < nrec; k++)
+      if (rec_key_cmp(&rec[k - 1], &rec[k]) == 0) {
+        fprintf(stderr, "flow: two records hold one key\n");
+        bad = 1;
+      }
+  }
+  if (!bad && (st.packets != assigned || st.no_key != none)) {
+    fprintf(stderr, "flow: stats packets %llu/%llu no_key %llu/%llu\n",
+            (unsigned long long)st.packets, (unsigned long long)assigned,
+            (unsigned long long)st.no_key, (unsigned long long)none);
+    bad = 1;
+  }
+  *flows_out = nrec;
+  CHECK(gpd_flow_destroy(ft));
+  HCHECK(hipFree(d_id));
+  free(id), free(rec), free(ridx), free(pk), free(by), free(lo), free(hi);
+  return bad;
+}
+
+/* The batch as a little-endian microsecond pcap file (pcapgo/write.go:32-34 header). */
+static uint8_t *make_pcap(const uint8_t *data, const uint32_t *off, const uint32_t *cap,
+                          uint64_t n, uint64_t *len) {
+  uint64_t total = GPD_PCAP_HEADER_BYTES, snap = 0;
+  for (uint64_t i = 0; i < n; i++) {
+    total += GPD_PCAP_RECORD_BYTES + cap[i];
+    if (cap[i] > snap) snap = cap[i];
+  }
+  uint8_t *b = calloc(total + 64, 1);
+  const uint32_t h[6] = {GPD_PCAP_MAGIC_MICRO, 2 | (4u << 16), 0, 0, (uint32_t)snap + 1, 1};
+  memcpy(b, h, 24);
+  uint64_t p = GPD_PCAP_HEADER_BYTES;
+  for (uint64_t i = 0; i < n; i++) {
+    const uint32_t r[4] = {(uint32_t)i, 7, cap[i], cap[i]};
+    memcpy(b + p, r, 16);
+    memcpy(b + p + 16, data + off[i], cap[i]);
+    p += 16 + cap[i];
+  }
+  *len = total;
+  return b;
 }
 
 int main(int argc, char **argv) {
@@ -150,10 +264,29 @@ int main(int argc, char **argv) {
   gpo_decode_batch(data, off, cap, n, GPD_LT_ETHERNET, cfg.decoders, cfg.options, &t, ov.status,
                    ov.layers, ov.net_hash, ov.tp_hash, ov.csum, ov.hdr_off, NULL, 8);
 
+  /* 4. the same packets as a pcap capture */
+  res_t pv = res_alloc(n);
+  uint64_t plen = 0, pn = 0, pnext = 0;
+  int pstop = -1;
+  uint8_t *cap_file = make_pcap(data, off, cap, n, &plen);
+  gpd_result pr = {pv.status, pv.layers, pv.net_hash, pv.tp_hash, pv.csum, NULL, pv.hdr_off};
+  CHECK(gpd_decode_pcap(ctx, cap_file, plen, n, &pr, &pn, &pnext, &pstop, 4));
   int bad = res_cmp("gpd_decode vs oracle", &dv, &ov, n) | res_cmp("gpd_decode_host vs oracle", &hv, &ov, n);
+  if (pn != n || pnext != plen || (n > 0 && pstop != GPD_PCAP_STOP_LIMIT && pstop != GPD_PCAP_STOP_EOF)) {
+    fprintf(stderr, "gpd_decode_pcap: n %llu/%llu next %llu/%llu stop %d\n", (unsigned long long)pn,
+            (unsigned long long)n, (unsigned long long)pnext, (unsigned long long)plen, pstop);
+    bad = 1;
+  } else {
+    bad |= res_cmp("gpd_decode_pcap vs oracle", &pv, &ov, n);
+  }
+
+  /* 5. the device results feed the flow table */
+  uint64_t flows = 0;
+  if (!bad && n > 0) bad |= check_flows(ctx, s, &db, &dr, data, off, cap, ov.hdr_off, n, &flows);
+
   CHECK(gpd_ctx_destroy(ctx));
   HCHECK(hipStreamDestroy(s));
   if (bad) return 1;
-  printf("abi_host ok %llu\n", (unsigned long long)n);
+  printf("abi_host ok %llu %llu\n", (unsigned long long)n, (unsigned long long)flows);
   return 0;
 }

@@ -90,7 +90,8 @@ def test_ctx_create_fails_loudly_without_device():
 def test_c_host_program_on_the_abi(tmp_path):
     """tests/c/abi_host: a plain C program (no Python, no torch in its process — the cgo case)
     decodes through gpd_decode on its own hipMalloc'ed buffers and stream and through
-    gpd_decode_host; both must equal the oracle bit for bit."""
+    gpd_decode_host and gpd_decode_pcap (the same packets as a capture file); all must equal the
+    oracle bit for bit, and the device results must build a consistent flow table."""
     import golden_cases as G
     from gopacket_amd import synth
     from gopacket_amd.batch import PacketBatch
@@ -111,4 +112,6 @@ def test_c_host_program_on_the_abi(tmp_path):
             fh.write(b.caplen.astype(np.uint32).tobytes())
         r = subprocess.run([exe, str(f)], capture_output=True, text=True, timeout=90)
         assert r.returncode == 0, r.stdout + r.stderr
-        assert r.stdout.strip() == f"abi_host ok {b.n}"
+        words = r.stdout.split()
+        assert words[:3] == ["abi_host", "ok", str(b.n)], r.stdout
+        assert int(words[3]) > 100, r.stdout  # the mixed traffic holds many TCP/UDP flows
