@@ -175,10 +175,27 @@ def bench_flows(parser, dev_batch, n, args, stream, local):
             ins.append(e[1].elapsed_time(e[2]))
     st = ft.Stats(stream)
     ms = float(np.mean(ins))
-    return {"diag": "F3 flow table (not the metric)", "packets": n, "insert_ms": round(ms, 4),
-            "insert_Mpackets_per_s": round(n / ms / 1e3, 1), "reset_ms": round(float(np.mean(rst)), 4),
-            "capacity": st["capacity"], "flows": st["flows"], "keyed_packets": st["packets"],
-            "collisions": st["collisions"], "full": st["full"]}
+    out = {"diag": "F3 flow table (not the metric)", "packets": n, "insert_ms": round(ms, 4),
+           "insert_Mpackets_per_s": round(n / ms / 1e3, 1), "reset_ms": round(float(np.mean(rst)), 4),
+           "capacity": st["capacity"], "flows": st["flows"], "keyed_packets": st["packets"],
+           "collisions": st["collisions"], "full": st["full"]}
+    # the flow-affine sharded table (one table per rank, key records exchanged all-to-all):
+    # host clock per phase, synchronised; with one rank the exchange is skipped
+    sft = FL.ShardedFlowTable(parser, cap)
+    rank = int(os.environ.get("RANK", "0"))
+    phases = []
+    for k in range(steps + 1):
+        sft.table.Reset(stream)
+        torch.cuda.synchronize(local)
+        sft.Insert(dev_batch, res, index_base=rank * n, stream=stream)
+        if k:
+            phases.append(sft.last_ms)
+    ph = {key: round(float(np.mean([p[key] for p in phases])), 4) for key in phases[0]}
+    tot = sum(ph.values())
+    out["sharded"] = {"ranks": sft.world, "phase_ms": ph, "total_ms": round(tot, 4),
+                      "Mpackets_per_s_per_rank": round(n / tot / 1e3, 1),
+                      "flows_on_rank": sft.Stats(stream)["flows"]}
+    return out
 
 
 def bench_tpv3(parser, batch, args):

@@ -17,6 +17,10 @@
 // The per-flow counters are device atomics.  A second launch compares every packet's key
 // with its record's stored key (visible after the launch boundary), so a fingerprint
 // collision is caught and reported instead of silently merging two flows.
+// Sharding over GPUs (gpd_flow_keys / gpd_flow_insert_keys): the same key, gathered once,
+// travels as a 64-byte record to the rank its FastHash pair names; two passes (count per
+// owner, then scatter with wave-aggregated cursors) group the records by owner without a
+// sort, and the owner inserts records exactly as packets.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -33,6 +37,8 @@ static_assert(sizeof(gpd_flow_rec) == 80, "gpd_flow_rec layout (include/gpd_flow
 
 enum : uint32_t { FS_FLOWS = 0, FS_PACKETS, FS_NOKEY, FS_FULL, FS_COLL, FS_EXPORT, FS_WORDS = 8 };
 
+static_assert(sizeof(gpd_flow_key) == 64, "gpd_flow_key layout (include/gpd_flow.h)");
+
 struct FlowParams {
   const uint8_t *data;
   uint64_t data_len;
@@ -42,6 +48,12 @@ struct FlowParams {
   gpd_flow_rec *tab;
   uint64_t mask;  // capacity - 1
   unsigned long long *stats;
+  // sharding (gpd_flow_keys / gpd_flow_insert_keys)
+  const gpd_flow_key *keys;  // key records to insert (KEYS kernels)
+  const uint64_t *net_hash, *tp_hash;
+  gpd_flow_key *kout;         // partitioned key records (gpd_flow_keys)
+  unsigned long long *parts;  // [0, nparts): counts; [nparts, 2 nparts): scatter cursors
+  uint32_t nparts;
 };
 
 // The key of packet i as 10 words: src[16], dst[16], ports (raw wire bytes), types.  Returns
@@ -95,12 +107,33 @@ __device__ __forceinline__ void wave_count(unsigned long long *ctr, bool pred) {
     atomicAdd(ctr, (unsigned long long)__popcll(m));
 }
 
+// Key of item i: gathered from the packet bytes, or read from a key record (KEYS).
+template <bool KEYS>
+__device__ __forceinline__ bool item_key(const FlowParams &P, uint64_t i, uint32_t (&k)[10],
+                                         uint64_t &seq, uint32_t &caplen) {
+  if constexpr (KEYS) {
+    const gpd_flow_key &r = P.keys[i];
+#pragma unroll
+    for (int j = 0; j < 10; j++) k[j] = r.key[j];
+    seq = r.seq;
+    caplen = r.caplen;
+    return true;
+  } else {
+    seq = P.base + i;
+    caplen = P.caplen[i];
+    return flow_key(P, i, k);
+  }
+}
+
+template <bool KEYS>
 __global__ __launch_bounds__(kFlowThreads) void flow_insert_kernel(FlowParams P) {
   for (uint64_t i = blockIdx.x * (uint64_t)kFlowThreads + threadIdx.x; i - threadIdx.x < P.n;
        i += (uint64_t)gridDim.x * kFlowThreads) {
     const bool live = i < P.n;
     uint32_t k[10];
-    const bool keyed = live && flow_key(P, i, k);
+    uint64_t seq = 0;
+    uint32_t caplen = 0;
+    const bool keyed = live && item_key<KEYS>(P, i, k, seq, caplen);
     bool created = false, full = false;
     uint64_t s = 0;
     if (keyed) {
@@ -128,12 +161,11 @@ __global__ __launch_bounds__(kFlowThreads) void flow_insert_kernel(FlowParams P)
     }
     const bool counted = keyed && !full;
     if (counted) {
-      const uint64_t seq = P.base + i;
       gpd_flow_rec &r = P.tab[s];
       atomicMin(reinterpret_cast<unsigned long long *>(&r.first), (unsigned long long)seq);
       atomicMax(reinterpret_cast<unsigned long long *>(&r.last), (unsigned long long)seq);
       atomicAdd(reinterpret_cast<unsigned long long *>(&r.packets), 1ull);
-      atomicAdd(reinterpret_cast<unsigned long long *>(&r.bytes), (unsigned long long)P.caplen[i]);
+      atomicAdd(reinterpret_cast<unsigned long long *>(&r.bytes), (unsigned long long)caplen);
     }
     if (live) P.flow_id[i] = !keyed ? GPD_FLOW_NONE : full ? GPD_FLOW_FULL : (uint32_t)s;
     wave_count(P.stats + FS_FLOWS, created);
@@ -143,7 +175,8 @@ __global__ __launch_bounds__(kFlowThreads) void flow_insert_kernel(FlowParams P)
   }
 }
 
-// Second pass: every packet's key against its record's stored key.
+// Second pass: every item's key against its record's stored key.
+template <bool KEYS>
 __global__ __launch_bounds__(kFlowThreads) void flow_verify_kernel(FlowParams P) {
   for (uint64_t i = blockIdx.x * (uint64_t)kFlowThreads + threadIdx.x; i - threadIdx.x < P.n;
        i += (uint64_t)gridDim.x * kFlowThreads) {
@@ -151,7 +184,9 @@ __global__ __launch_bounds__(kFlowThreads) void flow_verify_kernel(FlowParams P)
     if (i < P.n) {
       const uint32_t id = P.flow_id[i];
       uint32_t k[10];
-      if (id < GPD_FLOW_FULL && flow_key(P, i, k)) {
+      uint64_t seq;
+      uint32_t caplen;
+      if (id < GPD_FLOW_FULL && item_key<KEYS>(P, i, k, seq, caplen)) {
         const gpd_flow_rec &r = P.tab[id];
         const uint32_t *w = reinterpret_cast<const uint32_t *>(r.src);
         bool same = k[9] == ((uint32_t)r.net_type | ((uint32_t)r.tp_type << 8) | ((uint32_t)r.addr_len << 16));
@@ -164,6 +199,135 @@ __global__ __launch_bounds__(kFlowThreads) void flow_verify_kernel(FlowParams P)
       }
     }
     wave_count(P.stats + FS_COLL, bad);
+  }
+}
+
+// Owner rank of a keyed packet: the high half of the two direction-symmetric FastHashes'
+// xor, scaled to [0, nparts) (doc.go:216-228 picks a worker by flow.FastHash()).
+__device__ __forceinline__ uint32_t flow_owner(const FlowParams &P, uint64_t i) {
+  const uint64_t h = P.net_hash[i] ^ P.tp_hash[i];
+  return (uint32_t)(((h >> 32) * (uint64_t)P.nparts) >> 32);
+}
+
+// Wave-aggregated claim of one slot of counter ctr[owner] (LDS) for every lane with `has`:
+// one LDS atomic per distinct owner in the wave; returns the lane's slot.
+__device__ __forceinline__ uint32_t wave_claim(uint32_t *ctr, bool has, uint32_t owner) {
+  const uint32_t lane = threadIdx.x & 63u;
+  uint64_t todo = __ballot(has);
+  uint32_t slot = 0;
+  while (todo) {
+    const uint32_t o = __builtin_amdgcn_readlane(owner, (int)__builtin_ctzll(todo));
+    const uint64_t m = __ballot(has && owner == o);
+    const int leader = (int)__builtin_ctzll(m);
+    uint32_t base = 0;
+    if (lane == (uint32_t)leader) base = atomicAdd(ctr + o, (uint32_t)__popcll(m));
+    base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
+    if (has && owner == o)
+      slot = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    todo &= ~m;
+  }
+  return slot;
+}
+
+// gpd_flow_keys, pass 1: each workgroup counts its packets per owner in LDS and writes the
+// counts owner-major (parts[p * G + b]), so that one exclusive scan of the whole array gives
+// every (owner, workgroup) its output range.  No global atomics.
+__global__ __launch_bounds__(kFlowThreads) void flow_part_count_kernel(FlowParams P) {
+  __shared__ uint32_t cnt[GPD_FLOW_MAX_PARTS];
+  for (uint32_t p = threadIdx.x; p < P.nparts; p += kFlowThreads) cnt[p] = 0;
+  __syncthreads();
+  for (uint64_t i = blockIdx.x * (uint64_t)kFlowThreads + threadIdx.x; i - threadIdx.x < P.n;
+       i += (uint64_t)gridDim.x * kFlowThreads) {
+    uint32_t k[10];
+    const bool keyed = i < P.n && flow_key(P, i, k);
+    (void)wave_claim(cnt, keyed, keyed ? flow_owner(P, i) : 0u);
+  }
+  __syncthreads();
+  for (uint32_t p = threadIdx.x; p < P.nparts; p += kFlowThreads)
+    P.parts[(uint64_t)p * gridDim.x + blockIdx.x] = cnt[p];
+}
+
+// Pass 2 (one workgroup): exclusive scan of the L = nparts * G counts in place; parts[L] =
+// the total, and parts[L + 1 + p] = owner p's total.
+__global__ __launch_bounds__(1024) void flow_part_scan_kernel(unsigned long long *parts, uint64_t L,
+                                                              uint32_t nparts, uint32_t G) {
+  __shared__ unsigned long long sums[1024];
+  const uint64_t per = (L + 1023) / 1024, lo = threadIdx.x * per, hi = min(L, lo + per);
+  unsigned long long s = 0;
+  for (uint64_t j = lo; j < hi; j++) s += parts[j];
+  sums[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long run = 0;
+    for (int t = 0; t < 1024; t++) {
+      const unsigned long long v = sums[t];
+      sums[t] = run;
+      run += v;
+    }
+    parts[L] = run;
+  }
+  __syncthreads();
+  unsigned long long run = sums[threadIdx.x];
+  for (uint64_t j = lo; j < hi; j++) {
+    const unsigned long long v = parts[j];
+    parts[j] = run;
+    run += v;
+  }
+  __syncthreads();
+  for (uint32_t p = threadIdx.x; p < nparts; p += 1024)
+    parts[L + 1 + p] = parts[(uint64_t)(p + 1) * G < L ? (uint64_t)(p + 1) * G : L] - parts[(uint64_t)p * G];
+}
+
+// Pass 3: each keyed packet's record at its (owner, workgroup) range start + an LDS slot.
+// Same grid and packet-to-workgroup mapping as pass 1.
+__global__ __launch_bounds__(kFlowThreads) void flow_part_scatter_kernel(FlowParams P) {
+  __shared__ uint32_t cur[GPD_FLOW_MAX_PARTS];
+  __shared__ unsigned long long start[GPD_FLOW_MAX_PARTS];
+  for (uint32_t p = threadIdx.x; p < P.nparts; p += kFlowThreads) {
+    cur[p] = 0;
+    start[p] = P.parts[(uint64_t)p * gridDim.x + blockIdx.x];
+  }
+  __syncthreads();
+  for (uint64_t i = blockIdx.x * (uint64_t)kFlowThreads + threadIdx.x; i - threadIdx.x < P.n;
+       i += (uint64_t)gridDim.x * kFlowThreads) {
+    uint32_t k[10];
+    const bool keyed = i < P.n && flow_key(P, i, k);
+    const uint32_t o = keyed ? flow_owner(P, i) : 0u;
+    const uint32_t slot = wave_claim(cur, keyed, o);
+    if (keyed) {
+      gpd_flow_key r;
+#pragma unroll
+      for (int j = 0; j < 10; j++) r.key[j] = k[j];
+      r.caplen = P.caplen[i];
+      r.owner = o;
+      r.seq = P.base + i;
+      r.fp = fingerprint(k);
+      P.kout[start[o] + slot] = r;
+    }
+  }
+}
+
+// gpd_flow_key_ids: every packet's (owner, flow id) from the key records it sent and the ids
+// their owners returned (sent record j <-> ids[j]).
+__global__ __launch_bounds__(kFlowThreads) void flow_ids_fill_kernel(int32_t *owner, uint32_t *flow_id,
+                                                                     uint64_t n) {
+  for (uint64_t i = blockIdx.x * (uint64_t)kFlowThreads + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * kFlowThreads) {
+    owner[i] = -1;
+    flow_id[i] = GPD_FLOW_NONE;
+  }
+}
+__global__ __launch_bounds__(kFlowThreads) void flow_ids_scatter_kernel(const gpd_flow_key *keys, uint64_t m,
+                                                                        const uint32_t *ids, uint64_t base,
+                                                                        uint64_t n, int32_t *owner,
+                                                                        uint32_t *flow_id) {
+  for (uint64_t j = blockIdx.x * (uint64_t)kFlowThreads + threadIdx.x; j < m;
+       j += (uint64_t)gridDim.x * kFlowThreads) {
+    const uint64_t i = keys[j].seq - base;
+    if (i < n) {
+      owner[i] = (int32_t)keys[j].owner;
+      flow_id[i] = ids[j];
+    }
   }
 }
 
@@ -200,6 +364,8 @@ struct gpd_flowtable {
   gpd_flow_rec *tab = nullptr;
   uint64_t cap = 0;
   unsigned long long *stats = nullptr;  // FS_WORDS counters
+  unsigned long long *parts = nullptr;  // gpd_flow_keys: nparts x grid counts (+ totals), grown on use
+  uint64_t parts_words = 0;
 };
 
 #define FLOW_TRY(expr)                                                                      \
@@ -268,12 +434,90 @@ int gpd_flow_insert(gpd_flowtable *ft, const gpd_batch *in, const gpd_result *re
     return gpd::set_error(GPD_ERR_INVALID, "gpd_flow_insert: null batch array");
   FLOW_TRY(hipSetDevice(ft->device));
   gpd::FlowParams P{in->data, in->data_len, in->offset, in->caplen, res->status, res->hdr_off,
-                    flow_id, in->n, index_base, ft->tab, ft->cap - 1, ft->stats};
+                    flow_id, in->n, index_base, ft->tab, ft->cap - 1, ft->stats,
+                    nullptr, nullptr, nullptr, nullptr, nullptr, 0};
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid(grid_for(in->n, ft->num_cus)), block(gpd::kFlowThreads);
-  hipLaunchKernelGGL(gpd::flow_insert_kernel, grid, block, 0, s, P);
+  hipLaunchKernelGGL(gpd::flow_insert_kernel<false>, grid, block, 0, s, P);
   FLOW_TRY(hipGetLastError());
-  hipLaunchKernelGGL(gpd::flow_verify_kernel, grid, block, 0, s, P);
+  hipLaunchKernelGGL(gpd::flow_verify_kernel<false>, grid, block, 0, s, P);
+  FLOW_TRY(hipGetLastError());
+  return GPD_OK;
+}
+
+int gpd_flow_keys(gpd_flowtable *ft, const gpd_batch *in, const gpd_result *res, uint32_t nparts,
+                  uint64_t index_base, gpd_flow_key *keys, uint64_t *part_count, void *stream) {
+  if (!ft || !in || !res || !part_count || (in->n && !keys))
+    return gpd::set_error(GPD_ERR_INVALID, "gpd_flow_keys: null argument");
+  if (nparts == 0 || nparts > GPD_FLOW_MAX_PARTS)
+    return gpd::set_error(GPD_ERR_INVALID, "gpd_flow_keys: nparts %u outside [1, %d]", nparts,
+                          GPD_FLOW_MAX_PARTS);
+  if (!res->status || !res->hdr_off || !res->net_hash || !res->tp_hash)
+    return gpd::set_error(GPD_ERR_INVALID,
+                          "gpd_flow_keys: the results need status, hdr_off, net_hash and tp_hash");
+  for (uint32_t p = 0; p < nparts; p++) part_count[p] = 0;
+  if (in->n == 0) return GPD_OK;
+  if (!in->data || !in->offset || !in->caplen)
+    return gpd::set_error(GPD_ERR_INVALID, "gpd_flow_keys: null batch array");
+  FLOW_TRY(hipSetDevice(ft->device));
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid(grid_for(in->n, ft->num_cus)), block(gpd::kFlowThreads);
+  const uint64_t L = (uint64_t)nparts * grid.x, words = L + 1 + nparts;
+  if (ft->parts_words < words) {
+    if (ft->parts) FLOW_TRY(hipFree(ft->parts));
+    ft->parts = nullptr;
+    ft->parts_words = 0;
+    FLOW_TRY(hipMalloc(&ft->parts, words * sizeof(unsigned long long)));
+    ft->parts_words = words;
+  }
+  gpd::FlowParams P{in->data, in->data_len, in->offset, in->caplen, res->status, res->hdr_off,
+                    nullptr, in->n, index_base, ft->tab, ft->cap - 1, ft->stats,
+                    nullptr, res->net_hash, res->tp_hash, keys, ft->parts, nparts};
+  hipLaunchKernelGGL(gpd::flow_part_count_kernel, grid, block, 0, s, P);
+  FLOW_TRY(hipGetLastError());
+  hipLaunchKernelGGL(gpd::flow_part_scan_kernel, dim3(1), dim3(1024), 0, s, ft->parts, L, nparts, grid.x);
+  FLOW_TRY(hipGetLastError());
+  hipLaunchKernelGGL(gpd::flow_part_scatter_kernel, grid, block, 0, s, P);
+  FLOW_TRY(hipGetLastError());
+  std::vector<unsigned long long> h(nparts);
+  FLOW_TRY(hipMemcpyAsync(h.data(), ft->parts + L + 1, nparts * sizeof(unsigned long long),
+                          hipMemcpyDeviceToHost, s));
+  FLOW_TRY(hipStreamSynchronize(s));
+  for (uint32_t p = 0; p < nparts; p++) part_count[p] = h[p];
+  return GPD_OK;
+}
+
+int gpd_flow_key_ids(gpd_flowtable *ft, const gpd_flow_key *keys, uint64_t m, const uint32_t *ids,
+                     uint64_t index_base, uint64_t n, int32_t *owner, uint32_t *flow_id, void *stream) {
+  if (!ft || (m && (!keys || !ids)) || (n && (!owner || !flow_id)))
+    return gpd::set_error(GPD_ERR_INVALID, "gpd_flow_key_ids: null argument");
+  if (n == 0) return GPD_OK;
+  FLOW_TRY(hipSetDevice(ft->device));
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(gpd::flow_ids_fill_kernel, dim3(grid_for(n, ft->num_cus)), dim3(gpd::kFlowThreads),
+                     0, s, owner, flow_id, n);
+  FLOW_TRY(hipGetLastError());
+  if (m) {
+    hipLaunchKernelGGL(gpd::flow_ids_scatter_kernel, dim3(grid_for(m, ft->num_cus)),
+                       dim3(gpd::kFlowThreads), 0, s, keys, m, ids, index_base, n, owner, flow_id);
+    FLOW_TRY(hipGetLastError());
+  }
+  return GPD_OK;
+}
+
+int gpd_flow_insert_keys(gpd_flowtable *ft, const gpd_flow_key *keys, uint64_t n,
+                         uint32_t *flow_id, void *stream) {
+  if (!ft || (n && (!keys || !flow_id)))
+    return gpd::set_error(GPD_ERR_INVALID, "gpd_flow_insert_keys: null argument");
+  if (n == 0) return GPD_OK;
+  FLOW_TRY(hipSetDevice(ft->device));
+  gpd::FlowParams P{nullptr, 0, nullptr, nullptr, nullptr, nullptr, flow_id, n, 0, ft->tab,
+                    ft->cap - 1, ft->stats, keys, nullptr, nullptr, nullptr, nullptr, 0};
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid(grid_for(n, ft->num_cus)), block(gpd::kFlowThreads);
+  hipLaunchKernelGGL(gpd::flow_insert_kernel<true>, grid, block, 0, s, P);
+  FLOW_TRY(hipGetLastError());
+  hipLaunchKernelGGL(gpd::flow_verify_kernel<true>, grid, block, 0, s, P);
   FLOW_TRY(hipGetLastError());
   return GPD_OK;
 }
@@ -340,6 +584,7 @@ int gpd_flow_destroy(gpd_flowtable *ft) {
   (void)hipSetDevice(ft->device);
   if (ft->tab) (void)hipFree(ft->tab);
   if (ft->stats) (void)hipFree(ft->stats);
+  if (ft->parts) (void)hipFree(ft->parts);
   delete ft;
   return GPD_OK;
 }

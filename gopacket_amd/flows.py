@@ -89,3 +89,127 @@ class FlowTable:
 
 def NewFlowTable(parser: DecodingLayerParser, capacity: int) -> FlowTable:
     return FlowTable(parser, capacity)
+
+
+# ---------------------------------------------------------------- flow-affine sharding
+FLOW_KEY_DTYPE = np.dtype([("key", "<u4", (10,)), ("caplen", "<u4"), ("owner", "<u4"),
+                           ("seq", "<u8"), ("fp", "<u8")])
+assert FLOW_KEY_DTYPE.itemsize == 64
+KEY_WORDS = 8  # a key record as int64 words: the unit the exchange moves
+
+
+def exchange_keys(keys, counts, group=None):
+    """The all-to-all of key records: `keys` is an int64 tensor [m, 8] grouped
+    by owner rank, `counts` the records per owner (host ints).  Returns (received records
+    [r, 8], records received from each rank).  On a `gloo` group the records travel through
+    host memory; on `nccl` (RCCL over xGMI) they stay in HBM."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    assert len(counts) == world
+    host = dist.get_backend(group) == "gloo"
+    dev = keys.device
+    send_counts = torch.tensor([int(c) for c in counts], dtype=torch.int64)
+    recv_counts = torch.empty(world, dtype=torch.int64)
+    if host:
+        dist.all_to_all_single(recv_counts, send_counts, group=group)
+    else:
+        rc = recv_counts.to(dev)
+        dist.all_to_all_single(rc, send_counts.to(dev), group=group)
+        recv_counts = rc.cpu()
+    rcv = [int(c) for c in recv_counts]
+    src = keys.cpu() if host else keys
+    out = torch.empty((sum(rcv), KEY_WORDS), dtype=torch.int64, device=src.device)
+    dist.all_to_all_single(out, src.contiguous(), output_split_sizes=rcv,
+                           input_split_sizes=[int(c) for c in counts], group=group)
+    return (out.to(dev) if host else out), rcv
+
+
+def return_ids(ids, recv_counts, send_counts, group=None):
+    """The reverse all-to-all: each rank's flow ids for the records it received go back to the
+    senders, in the order they were sent."""
+    import torch
+    import torch.distributed as dist
+    host = dist.get_backend(group) == "gloo"
+    dev = ids.device
+    src = ids.cpu() if host else ids
+    out = torch.empty(sum(int(c) for c in send_counts), dtype=ids.dtype, device=src.device)
+    dist.all_to_all_single(out, src.contiguous(), output_split_sizes=[int(c) for c in send_counts],
+                           input_split_sizes=[int(c) for c in recv_counts], group=group)
+    return out.to(dev) if host else out
+
+
+class ShardedFlowTable:
+    """The flow table sharded over the ranks of a torch.distributed group, one table per GPU.
+
+    The reference fans packets out to workers by flow hash (doc.go:216-228,
+    `flow.FastHash() % numWorkers`); here every rank decodes its own packets, turns the keyed
+    ones into 64-byte key records grouped by owning rank (gpd_flow_keys), exchanges them with
+    one all-to-all (RCCL over xGMI on `nccl`), and inserts what it received into its table
+    (gpd_flow_insert_keys).  Each flow, both directions of a conversation included, lives on
+    exactly one rank.  Insert returns each local packet's (owner rank, flow record index on
+    that rank); Export lists this rank's flows."""
+
+    def __init__(self, parser: DecodingLayerParser, capacity: int, group=None):
+        import torch.distributed as dist
+        self.table = FlowTable(parser, capacity)
+        self.group = group
+        self.single = not (dist.is_available() and dist.is_initialized())  # one rank, no exchange
+        self.world = 1 if self.single else dist.get_world_size(group)
+        self.rank = 0 if self.single else dist.get_rank(group)
+        self.last_ms = {}  # host-clock phases of the last Insert (synchronised), for diagnostics
+
+    def Insert(self, dbatch: DeviceBatch, dres: DeviceResult, index_base: int = 0, stream=None):
+        """Partition, exchange, insert (synchronous).  Returns int32 device tensors (owner rank
+        per packet, -1 without a key; flow record index on the owner, GPD_FLOW_* as uint32)."""
+        import time
+        torch = _torch()
+        t = self.table
+        if dres.hdr_off is None:
+            raise ValueError("ShardedFlowTable.Insert needs a DeviceResult with hdr_off")
+        dev = dres.status.device
+        t0 = time.perf_counter()
+        keys = torch.empty((max(dbatch.n, 1), KEY_WORDS), dtype=torch.int64, device=dev)
+        counts = (C.c_uint64 * self.world)()
+        b, r = dbatch.c_batch(), dres.c_result()
+        check(lib.gpd_flow_keys(t.h, C.byref(b), C.byref(r), self.world, int(index_base),
+                                C.c_void_p(keys.data_ptr()), counts, t._stream(stream)), "gpd_flow_keys")
+        send = [int(c) for c in counts]
+        m = sum(send)
+        t1 = time.perf_counter()
+        if self.single:
+            recv, rcv = keys[:m], send
+        else:
+            recv, rcv = exchange_keys(keys[:m], send, self.group)
+        t2 = time.perf_counter()
+        ids = torch.empty(max(recv.shape[0], 1), dtype=torch.int32, device=dev)
+        check(lib.gpd_flow_insert_keys(t.h, C.c_void_p(recv.data_ptr()), int(recv.shape[0]),
+                                       C.c_void_p(ids.data_ptr()), t._stream(stream)),
+              "gpd_flow_insert_keys")
+        if stream is not None:
+            stream.synchronize()
+        torch.cuda.synchronize(dev)
+        t3 = time.perf_counter()
+        back = ids[:m] if self.single else return_ids(ids[:recv.shape[0]], rcv, send, self.group)
+        owner = torch.empty(dbatch.n, dtype=torch.int32, device=dev)
+        flow_id = torch.empty(dbatch.n, dtype=torch.int32, device=dev)
+        check(lib.gpd_flow_key_ids(t.h, C.c_void_p(keys.data_ptr()), m, C.c_void_p(back.data_ptr()),
+                                   int(index_base), dbatch.n, C.c_void_p(owner.data_ptr()),
+                                   C.c_void_p(flow_id.data_ptr()), t._stream(stream)), "gpd_flow_key_ids")
+        torch.cuda.synchronize(dev)
+        t4 = time.perf_counter()
+        self.last_ms = {"keys": (t1 - t0) * 1e3, "exchange": (t2 - t1) * 1e3,
+                        "insert": (t3 - t2) * 1e3, "return": (t4 - t3) * 1e3}
+        return owner, flow_id
+
+    def Stats(self, stream=None) -> dict:
+        return self.table.Stats(stream)
+
+    def Export(self, max_flows: Optional[int] = None, stream=None):
+        return self.table.Export(max_flows, stream)
+
+
+def flow_owner(net_hash, tp_hash, nparts: int):
+    """The owner rank gpd_flow_keys assigns (include/gpd_flow.h), for host-side checks."""
+    h = (np.asarray(net_hash, np.uint64) ^ np.asarray(tp_hash, np.uint64)) >> np.uint64(32)
+    return ((h * np.uint64(nparts)) >> np.uint64(32)).astype(np.uint32)

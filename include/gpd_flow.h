@@ -88,6 +88,45 @@ int gpd_flow_export(gpd_flowtable *ft, gpd_flow_rec *out, uint32_t *rec_index, u
                     uint64_t *n, void *stream);
 int gpd_flow_destroy(gpd_flowtable *ft);
 
+/* ---- flow-affine sharding over several GPUs ----
+ * The reference's fan-out idiom sends every packet of a flow to one worker picked by the
+ * flow's FastHash (doc.go:216-228: "flow.FastHash() % numWorkers").  With one table per GPU,
+ * each rank turns its decoded packets into 64-byte key records grouped by owning rank
+ * (gpd_flow_keys), the ranks exchange them with one all-to-all, and each rank inserts the
+ * records it received into its own table (gpd_flow_insert_keys): every flow lives on exactly
+ * one rank and both directions of a conversation on the same one.
+ * owner = ((NetworkFlow().FastHash() ^ TransportFlow().FastHash()) >> 32) * nparts >> 32
+ * (both hashes are direction-symmetric, flows.go:167-174). */
+typedef struct gpd_flow_key {
+  uint32_t key[10];  /* src[16], dst[16], ports[4] as raw bytes; net_type | tp_type << 8 | addr_len << 16 */
+  uint32_t caplen;   /* the packet's captured length */
+  uint32_t owner;    /* the rank that owns the flow */
+  uint64_t seq;      /* packet sequence number: index_base + the packet's index in its batch */
+  uint64_t fp;       /* the key's fingerprint (the table's slot hash) */
+} gpd_flow_key;      /* 64 B */
+
+#define GPD_FLOW_MAX_PARTS 1024
+
+/* Key records of every packet of a decoded device batch that has a network + transport pair,
+ * grouped by owner: partition p occupies keys[start_p, start_p + part_count[p]) with start_p
+ * the sum of the counts below p.  `res` needs status, hdr_off, net_hash and tp_hash (decode
+ * without GPD_OPT_NO_FLOW_HASH); `keys` (device) holds in->n records; part_count (host,
+ * nparts entries) is filled when the call returns (it synchronises `stream`: the counts size
+ * the exchange).  Order within a partition is unspecified.  1 <= nparts <= GPD_FLOW_MAX_PARTS. */
+int gpd_flow_keys(gpd_flowtable *ft, const gpd_batch *in, const gpd_result *res, uint32_t nparts,
+                  uint64_t index_base, gpd_flow_key *keys, uint64_t *part_count, void *stream);
+/* Find-or-create the flow of every key record (device array of n), as gpd_flow_insert does for
+ * packets; flow_id[n] receives each record's index in this table (or a GPD_FLOW_* value).
+ * Asynchronous on `stream`. */
+int gpd_flow_insert_keys(gpd_flowtable *ft, const gpd_flow_key *keys, uint64_t n,
+                         uint32_t *flow_id, void *stream);
+/* Back on the sending rank: given the m key records it sent (gpd_flow_keys' order) and the flow
+ * ids their owners returned for them (ids[j] for keys[j]), fill owner[n] (the owning rank, -1
+ * for a packet without a key) and flow_id[n] (the record index on the owner, GPD_FLOW_NONE
+ * without a key) for the n packets of the batch.  Device arrays; asynchronous on `stream`. */
+int gpd_flow_key_ids(gpd_flowtable *ft, const gpd_flow_key *keys, uint64_t m, const uint32_t *ids,
+                     uint64_t index_base, uint64_t n, int32_t *owner, uint32_t *flow_id, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -86,3 +86,63 @@ def test_shard_matches_single_rank_decode(two_ranks):
     res = O.decode(batch, ext=False, nthreads=2)
     assert np.array_equal(res.net_hash, r[1]["net_hash"])
     assert np.array_equal(res.status, r[1]["status"])
+
+
+# ---------------------------------------------------------------- flow-affine sharding (F3, §8(e))
+def _key_records(batch, res, base, world):
+    """Host-built key records (the layout gpd_flow_keys writes), grouped by owner rank."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import flow_ref as F
+    from gopacket_amd import flows as FL
+    keyed, keys = F.flow_keys(batch, res)
+    owner = FL.flow_owner(res.net_hash, res.tp_hash, world)
+    idx = np.nonzero(keyed)[0]
+    idx = idx[np.argsort(owner[idx], kind="stable")]
+    rec = np.zeros(len(idx), FL.FLOW_KEY_DTYPE)
+    rec["key"] = keys[idx].view("<u4").reshape(-1, 10)
+    rec["caplen"] = batch.caplen[idx]
+    rec["owner"] = owner[idx]
+    rec["seq"] = base + idx
+    counts = np.bincount(owner[idx], minlength=world)
+    return rec, counts
+
+
+def _xchg_worker(rank, world, port, out_dir):
+    import oracle_ref as O
+    from gopacket_amd import flows as FL
+    from gopacket_amd import synth
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    try:
+        batch = synth.make_mixed(700 + 150 * rank, seed=0x5EED0100 + rank)
+        res = O.decode(batch, 17, 0xFFF, ext=False)
+        rec, counts = _key_records(batch, res, rank << 32, world)
+        recv, rcv = FL.exchange_keys(torch.from_numpy(rec.view(np.int64).reshape(-1, 8)),
+                                     [int(c) for c in counts])
+        got = recv.numpy().reshape(-1).view(FL.FLOW_KEY_DTYPE)
+        ids = torch.from_numpy(((got["seq"] * 7) % 1000003).astype(np.int32))  # stand-in ids
+        back = FL.return_ids(ids, rcv, [int(c) for c in counts]).numpy()
+        np.savez(os.path.join(out_dir, f"x{rank}.npz"), sent=rec.view(np.uint8), got=got.view(np.uint8),
+                 rcv=np.array(rcv), counts=counts, back=back)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_flow_key_exchange_routes_every_record_to_its_owner(tmp_path):
+    """ShardedFlowTable's all-to-all on gloo, world 3: every rank receives exactly the key
+    records it owns from every rank, and the reverse exchange returns each record's id to its
+    sender in the order sent."""
+    from gopacket_amd import flows as FL
+    world = 3
+    mp.spawn(_xchg_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    r = [dict(np.load(tmp_path / f"x{k}.npz")) for k in range(world)]
+    sent = [x["sent"].view(FL.FLOW_KEY_DTYPE) for x in r]
+    got = [x["got"].view(FL.FLOW_KEY_DTYPE) for x in r]
+    for k in range(world):
+        assert (got[k]["owner"] == k).all()
+        want = np.concatenate([s[s["owner"] == k] for s in sent])
+        assert np.array_equal(np.sort(got[k]["seq"]), np.sort(want["seq"]))
+        assert int(r[k]["rcv"].sum()) == len(got[k])
+        assert np.array_equal(r[k]["back"], ((sent[k]["seq"] * 7) % 1000003).astype(np.int32))
+    # every owner receives some records, and a flow's two directions share an owner
+    assert all(len(g) > 0 for g in got)

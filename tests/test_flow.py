@@ -158,3 +158,112 @@ def test_flow_table_full():
     assert st["capacity"] == 64 and st["flows"] == 64
     assert st["full"] == int((fid == 0xFFFFFFFE).sum()) == batch.n - st["packets"]
     assert st["packets"] == int((fid < 64).sum())
+
+
+# ---------------------------------------------------------------- flow-affine sharding (§8(e))
+def test_flow_owner_is_direction_symmetric():
+    """Both directions of a conversation go to one owner: the owner is computed from
+    NetworkFlow().FastHash() ^ TransportFlow().FastHash(), both symmetric (flows.go:167-174)."""
+    from gopacket_amd import flows as FL
+    batch = _hot_batch(4000, 120, 4)
+    ref = O.decode(batch, L.LayerTypeEthernet, ALL, 0, ext=False)
+    keyed, keys = F.flow_keys(batch, ref)
+    for world in (2, 3, 8):
+        own = FL.flow_owner(ref.net_hash, ref.tp_hash, world)
+        by_key = {}
+        for i in np.nonzero(keyed)[0]:
+            k = keys[i]
+            rev = np.concatenate([k[16:32], k[0:16], k[34:36], k[32:34], k[36:40]]).tobytes()
+            by_key[k.tobytes()] = int(own[i])
+            if rev in by_key:
+                assert by_key[rev] == int(own[i])
+        assert set(own[keyed].tolist()) == set(range(world))
+
+
+def _global_batch():
+    pool = _hot_batch(6000, 400, 6)
+    mixed = synth.make_mixed(4000, seed=0x5EED0200)
+    return PacketBatch.from_packets([pool.packet(i) for i in range(pool.n)] +
+                                    [mixed.packet(i) for i in range(mixed.n)])
+
+
+def _shard_worker(rank, world, port, out_dir):
+    import torch
+    import torch.distributed as dist
+    from gopacket_amd import flows as FL
+    from gopacket_amd import parser as P
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    try:
+        full = _global_batch()
+        lo, hi = rank * full.n // world, (rank + 1) * full.n // world
+        shard = PacketBatch.from_packets([full.packet(i) for i in range(lo, hi)])
+        parser = P.NewDecodingLayerParser(L.LayerTypeEthernet, *[P.DECODER_BY_NAME[k]() for k in P.DECODER_BY_NAME])
+        db, dr = _decode_dev(parser, shard)
+        st = FL.ShardedFlowTable(parser, 1 << 14)
+        owner, fid = st.Insert(db, dr, index_base=lo)
+        torch.cuda.synchronize()
+        recs, idx = st.Export()
+        np.savez(os.path.join(out_dir, f"s{rank}.npz"), owner=owner.cpu().numpy(),
+                 fid=fid.cpu().numpy().view(np.uint32), recs=recs.view(np.uint8), idx=idx,
+                 stats=np.array(list(st.Stats().values()), np.uint64))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_sharded_flow_table_two_ranks():
+    """ShardedFlowTable with two ranks (gloo, both on the one GPU of the test box): every
+    flow lives on exactly one rank, the rank its FastHash pair names; the union of the two
+    tables equals the oracle's connection map of the whole batch; each packet's (owner, id)
+    names the record holding its key."""
+    import subprocess
+    import tempfile
+    from gopacket_amd import flows as FL
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        import socket
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        code = ("import sys; sys.path[:0] = [%r, %r]; import test_flow as T; "
+                "T._shard_worker(int(sys.argv[1]), %d, %d, %r)" % (ROOT, os.path.join(ROOT, "tests"),
+                                                                   world, port, d))
+        procs = [subprocess.Popen([sys.executable, "-c", code, str(r)], stdout=subprocess.PIPE,
+                                  stderr=subprocess.STDOUT, text=True) for r in range(world)]
+        outs = [p.communicate(timeout=100)[0] for p in procs]
+        assert all(p.returncode == 0 for p in procs), "\n".join(outs)
+        r = [dict(np.load(os.path.join(d, f"s{k}.npz"))) for k in range(world)]
+    full = _global_batch()
+    ref = O.decode(full, L.LayerTypeEthernet, ALL, 0, ext=False, nthreads=8)
+    flows_ref, per_ref = F.group(full, ref)
+    own_ref = FL.flow_owner(ref.net_hash, ref.tp_hash, world)
+    owner = np.concatenate([x["owner"] for x in r])
+    fid = np.concatenate([x["fid"] for x in r])
+    tables = []
+    for k, x in enumerate(r):
+        recs = x["recs"].view(FL.FLOW_REC_DTYPE)
+        tables.append({int(i): rec for i, rec in zip(x["idx"], recs)})
+        assert int(x["stats"][4]) == 0, "no fingerprint collisions"
+    seen = {}
+    for i, key in enumerate(per_ref):
+        if key is None:
+            assert owner[i] == -1 and fid[i] == 0xFFFFFFFF
+            continue
+        assert owner[i] == own_ref[i]
+        assert F.record_key(tables[owner[i]][int(fid[i])]) == key
+        seen.setdefault(key, (int(owner[i]), int(fid[i])))
+        assert seen[key] == (int(owner[i]), int(fid[i]))
+    union = {}
+    for k, t in enumerate(tables):
+        for rec in t.values():
+            key = F.record_key(rec)
+            assert key not in union, "a flow on two ranks"
+            union[key] = rec
+    assert set(union) == set(flows_ref)
+    for key, f in flows_ref.items():
+        rec = union[key]
+        assert (int(rec["first"]), int(rec["last"]), int(rec["packets"]), int(rec["bytes"])) == \
+            (f["first"], f["last"], f["packets"], f["bytes"])
+    assert all(len(t) > 0 for t in tables)
