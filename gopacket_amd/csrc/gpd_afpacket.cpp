@@ -49,7 +49,7 @@ inline uint32_t block_emits(const tpacket_hdr_v1 &bh, const tpacket3_hdr &p0) {
   return bh.num_pkts >= 1 ? bh.num_pkts : 1;
 }
 
-int walk_block(const gpd_tpv3_ring &R, const BlockPlan &B, const gpd_tpv3_pkts &pk) {
+int walk_block(const gpd_tpv3_ring &R, const BlockPlan &B, const gpd_tpv3_pkts &pk, uint32_t *off32) {
   const uint8_t *blk = R.base + (uint64_t)B.ring_block * R.block_size;
   const auto *desc = reinterpret_cast<const tpacket_block_desc *>(blk);
   const tpacket_hdr_v1 &bh = desc->hdr.bh1;
@@ -77,6 +77,7 @@ int walk_block(const gpd_tpv3_ring &R, const BlockPlan &B, const gpd_tpv3_pkts &
     if (data + h->tp_snaplen > R.block_size)
       return gpd::set_error(GPD_ERR_INVALID, "tpv3 block %u: frame outside the block", B.ring_block);
     pk.offset[j] = (uint64_t)B.ring_block * R.block_size + data;
+    if (off32) off32[j] = (uint32_t)pk.offset[j];  // rings below 4 GiB: a gpd_batch offset
     pk.caplen[j] = h->tp_snaplen;
     if (pk.wire_len) pk.wire_len[j] = h->tp_len;
     if (pk.ts_ns) pk.ts_ns[j] = (uint64_t)h->tp_sec * 1000000000ull + h->tp_nsec;
@@ -127,14 +128,14 @@ int plan_walk(const gpd_tpv3_ring *R, uint32_t first, uint32_t max_blocks, uint6
 }
 
 int run_walk(const gpd_tpv3_ring *R, const std::vector<BlockPlan> &plan, const gpd_tpv3_pkts &pk,
-             int nthreads) {
+             int nthreads, uint32_t *off32 = nullptr) {
   // nthreads <= 0: the machine's cores, at most 16 (blocks are few and cheap to walk)
   int T = nthreads > 0 ? nthreads : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
   T = (int)std::min<size_t>((size_t)T, plan.size());
   if (plan.size() < 8) T = 1;  // a thread per block costs more than walking a few blocks
   if (T <= 1) {
     for (const auto &b : plan) {
-      int rc = walk_block(*R, b, pk);
+      int rc = walk_block(*R, b, pk, off32);
       if (rc) return rc;
     }
     return GPD_OK;
@@ -143,7 +144,7 @@ int run_walk(const gpd_tpv3_ring *R, const std::vector<BlockPlan> &plan, const g
   std::vector<std::thread> th;
   for (int t = 0; t < T; t++)
     th.emplace_back([&, t] {
-      for (size_t b = t; b < plan.size() && rc[t] == GPD_OK; b += T) rc[t] = walk_block(*R, plan[b], pk);
+      for (size_t b = t; b < plan.size() && rc[t] == GPD_OK; b += T) rc[t] = walk_block(*R, plan[b], pk, off32);
     });
   for (auto &x : th) x.join();
   for (int r : rc)
@@ -196,18 +197,45 @@ int gpd_decode_tpv3(gpd_ctx *ctx, const gpd_tpv3_ring *ring, uint32_t first_bloc
   uint64_t n = 0;
   int rc = plan_walk(ring, first_block, max_blocks, max_n, plan, n);
   if (rc || plan.empty()) return rc;
-  std::vector<uint64_t> off(n);
-  std::vector<uint32_t> cap(n), tci(n);
+  // the walk writes straight into the caller's arrays where it has them
+  std::vector<uint64_t> off_own;
+  std::vector<uint32_t> cap_own, tci_own;
   gpd_tpv3_pkts pk = pk_out ? *pk_out : gpd_tpv3_pkts{};
-  pk.offset = off.data();
-  pk.caplen = cap.data();
-  pk.vlan_tci = tci.data();
-  rc = run_walk(ring, plan, pk, nthreads);
+  if (!pk.offset) {
+    off_own.resize(n);
+    pk.offset = off_own.data();
+  }
+  if (!pk.caplen) {
+    cap_own.resize(n);
+    pk.caplen = cap_own.data();
+  }
+  if (add_vlan_header && !pk.vlan_tci) {
+    tci_own.resize(n);
+    pk.vlan_tci = tci_own.data();
+  }
+  const uint64_t ring_bytes = (uint64_t)ring->block_size * ring->num_blocks;
+  // batch offsets for the ring as the buffer (kept per thread across calls: a capture loop
+  // calls again and again, and fresh pages cost more than the walk)
+  static thread_local std::vector<uint32_t> off32;
+  const bool direct = ring_bytes <= 0xFFFFFFF0ull;
+  if (direct && off32.size() < n) off32.resize(n);
+  rc = run_walk(ring, plan, pk, nthreads, direct ? off32.data() : nullptr);
   if (rc) return rc;
-  if (pk_out) {  // the caller's copies of the two arrays the decode needs for itself
-    if (pk_out->offset) memcpy(pk_out->offset, off.data(), n * 8);
-    if (pk_out->caplen) memcpy(pk_out->caplen, cap.data(), n * 4);
-    if (pk_out->vlan_tci) memcpy(pk_out->vlan_tci, tci.data(), n * 4);
+  const uint64_t *off = pk.offset;
+  const uint32_t *cap = pk.caplen, *tci = pk.vlan_tci;
+  bool tagging = false;
+  if (add_vlan_header)
+    for (uint64_t i = 0; i < n && !tagging; i++) tagging = tci[i] != 0;
+  if (!tagging && direct) {
+    // No frame needs a tag inserted: the ring itself is the batch buffer (offsets relative to
+    // its base) and the pipelined host path moves it — whole runs of frames straight from a
+    // registered ring, or the frames repacked in parallel — with two chunks in flight.
+    const gpd_batch hb{ring->base, ring_bytes, off32.data(), cap, n};
+    rc = gpd_decode_host(ctx, &hb, out);
+    if (rc) return rc;
+    *n_out = n;
+    *blocks_out = (uint32_t)plan.size();
+    return GPD_OK;
   }
   // device image: the walked blocks in walk order, then the VLAN-tagged copies
   const uint64_t B = ring->block_size, nb = plan.size();

@@ -297,15 +297,20 @@ class DecodingLayerParser:
         return out, k, err
 
     def DecodeTPv3(self, ring, max_n: int = 1 << 20, max_blocks: Optional[int] = None,
-                   add_vlan_header: bool = False, nthreads: int = 0):
+                   add_vlan_header: bool = False, nthreads: int = 0, out=None, ci=None):
         """Every packet of the user-owned blocks of a TPACKET_V3 ring (afpacket.TPv3Ring) from
         ring.offset on, decoded on the GPU where it lies (gpd_decode_tpv3).  The blocks are not
-        released.  Returns (BatchResult, CaptureInfo, blocks walked)."""
+        released.  Returns (BatchResult, CaptureInfo, blocks walked).  `out` (a BatchResult with
+        hdr_off) and `ci` (a CaptureInfo), both of at least max_n entries, are reused when given
+        — a capture loop keeps them across calls instead of touching fresh pages each time."""
         from .afpacket import CaptureInfo
-        ci = CaptureInfo.alloc(max_n)
-        res = BatchResult(np.zeros(max_n, np.uint32), np.zeros(max_n, np.uint64),
-                          np.zeros(max_n, np.uint64), np.zeros(max_n, np.uint64),
-                          np.zeros(max_n, np.uint32), None, np.zeros(max_n, np.uint32))
+        if ci is None:
+            ci = CaptureInfo.alloc(max_n)
+        res = out if out is not None else BatchResult(
+            np.zeros(max_n, np.uint32), np.zeros(max_n, np.uint64), np.zeros(max_n, np.uint64),
+            np.zeros(max_n, np.uint64), np.zeros(max_n, np.uint32), None, np.zeros(max_n, np.uint32))
+        if len(res.status) < max_n or res.hdr_off is None or len(ci.offset) < max_n:
+            raise ValueError("DecodeTPv3: out / ci must hold max_n entries (out with hdr_off)")
         r = GpdResult(res.status.ctypes.data, res.layers.ctypes.data, res.net_hash.ctypes.data,
                       res.tp_hash.ctypes.data, res.csum.ctypes.data, None, res.hdr_off.ctypes.data)
         n, nb = C.c_uint64(), C.c_uint32()
