@@ -241,10 +241,17 @@ def replay_pcap(parser, cap, n, total, threads):
     from gopacket_amd._lib import check, lib
     check(lib.gpd_host_register(parser.ctx().h, cap.ctypes.data, cap.nbytes), "gpd_host_register")
     try:
-        parser.DecodePcap(cap, nthreads=threads)  # warm: staging slots, streams
+        from gopacket_amd.results import BatchResult
+        # room for the most records the bytes could hold (the walk stays parallel without a
+        # bound); only the entries the records fill are ever touched
+        from gopacket_amd.batch import PAD
+        m = (cap.shape[0] - PAD - 24) // 16 + 1
+        out = BatchResult(np.zeros(m, np.uint32), np.zeros(m, np.uint64), np.zeros(m, np.uint64),
+                          np.zeros(m, np.uint64), np.zeros(m, np.uint32), None, np.zeros(m, np.uint32))
+        parser.DecodePcap(cap, nthreads=threads, out=out)  # warm: slots, streams, pages
         done, t0, reps = 0, time.perf_counter(), 0
         while done < total:
-            res, k, err = parser.DecodePcap(cap, nthreads=threads)
+            res, k, err = parser.DecodePcap(cap, nthreads=threads, out=out)
             assert err is None and k == n
             done += k
             reps += 1

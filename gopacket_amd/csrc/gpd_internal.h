@@ -113,6 +113,12 @@ struct Recs {  // one walked stretch of records
     ts.reserve(n);
   }
   size_t size() const { return pos.size(); }
+  void clear() {  // keeps the capacity: a walk reused across calls touches no fresh pages
+    pos.clear();
+    cap.clear();
+    wire.clear();
+    ts.clear();
+  }
   void push(uint64_t p, uint32_t c, uint32_t w, uint64_t t) {
     pos.push_back(p);
     cap.push_back(c);

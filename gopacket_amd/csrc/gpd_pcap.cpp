@@ -140,7 +140,11 @@ int default_threads() { return (int)std::min(16u, std::max(1u, std::thread::hard
 // segment record lists plus the in-order plan of slices that make up the walk.
 int pcap_walk(const uint8_t *buf, uint64_t len, const gpd_pcap_info &I, uint64_t pos, uint64_t max_n,
               int nthreads, PcapWalk &W) {
-  W = PcapWalk{};
+  for (auto &r : W.R) r.clear();  // a reused walk keeps its allocations
+  W.plan.clear();
+  W.n = W.next_pos = 0;
+  W.stop = W.threads = W.met = W.rewalks = 0;
+  W.a0 = W.a1 = 0;
   if (nthreads <= 0) nthreads = default_threads();
   const uint64_t span = len > pos ? len - pos : 0;
   const uint64_t kMinSeg = 4ull << 20;

@@ -763,17 +763,23 @@ int gpd_decode_pcap(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, uint64_t max
   gpd_pcap_info info;
   int rc = gpd_pcap_header(buf, len, &info);
   if (rc) return rc;
-  gpd::PcapWalk W;
+  // The walk and its flattened positions are kept per thread across calls (a replay or
+  // capture loop calls again and again; fresh pages for 24 B per record cost more than the
+  // walk itself).
+  static thread_local gpd::PcapWalk W;
+  static thread_local std::vector<uint64_t> rp;
+  static thread_local std::vector<uint32_t> rcap;
   const int wrc = gpd::pcap_walk(buf, len, info, GPD_PCAP_HEADER_BYTES, max_n, nthreads, W);
   std::string werr = wrc ? std::string(g_err) : std::string();
   const uint64_t n = W.n;
-  std::vector<uint64_t> rp(n);
-  std::vector<uint32_t> rcap(n);
+  if (rp.size() < n) {
+    rp.resize(n);
+    rcap.resize(n);
+  }
   gpd::pcap_emit(W, 0, nullptr, rp.data(), rcap.data(), nullptr, nullptr);
   *n_out = n;
   if (next_pos) *next_pos = W.next_pos;
   if (stop) *stop = W.stop;
-  W = gpd::PcapWalk{};  // free the walk
   HIP_TRY(hipSetDevice(ctx->device));
   const uint64_t kPkts = 1u << 20, kBytes = 256ull << 20;
   rc = alloc_slots(ctx, kBytes, kPkts, false);
@@ -796,10 +802,13 @@ int gpd_decode_pcap(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, uint64_t max
     const uint64_t m = j - i;
     const uint64_t end = rp[j - 1] + GPD_PCAP_RECORD_BYTES + rcap[j - 1];
     const uint64_t span = end - base;
-    for (uint64_t p = i; p < j; p++) {
-      s.h_off[p - i] = (uint32_t)(rp[p] + GPD_PCAP_RECORD_BYTES - base);
-      s.h_len[p - i] = rcap[p];
-    }
+    // (plain pointers: the worker threads would see their own thread_local vectors)
+    const uint64_t *RP = rp.data() + i;
+    const uint32_t *RC = rcap.data() + i;
+    par_for(m, 1u << 16, [&](uint64_t a, uint64_t b) {
+      for (uint64_t p = a; p < b; p++) s.h_off[p] = (uint32_t)(RP[p] + GPD_PCAP_RECORD_BYTES - base);
+      std::memcpy(s.h_len + a, RC + a, (b - a) * 4);
+    });
     const uint8_t *src = buf + base;
     if (!pinned) {
       par_memcpy(s.h_data, src, span, nthreads);

@@ -271,16 +271,22 @@ class DecodingLayerParser:
         return res
 
     def DecodePcap(self, cap: np.ndarray, max_n: Optional[int] = None, nthreads: int = 0,
-                   data_len: Optional[int] = None):
+                   data_len: Optional[int] = None, out: Optional[BatchResult] = None):
         """A whole in-memory capture (pcap.capture_array) through gpd_decode_pcap: records
         indexed natively, their raw bytes chunked host -> device, decoded, results back.
         Returns (BatchResult of the decoded records, number of records, error text or None —
-        the ReadPacketData loop's stop, pcapgo/read.go:120-137)."""
+        the ReadPacketData loop's stop, pcapgo/read.go:120-137).  `out` (a BatchResult with
+        hdr_off, at least max_n entries) is reused when given."""
         dl = cap.shape[0] - PAD if data_len is None else int(data_len)
         m = (dl - 24) // 16 + 1 if max_n is None else int(max_n)
-        res = BatchResult(np.zeros(m, np.uint32), np.zeros(m, np.uint64), np.zeros(m, np.uint64),
-                          np.zeros(m, np.uint64), np.zeros(m, np.uint32), None,
-                          np.zeros(m, np.uint32))
+        if out is not None:
+            if len(out.status) < m or out.hdr_off is None:
+                raise ValueError("DecodePcap: out must hold max_n entries, with hdr_off")
+            res = out
+        else:
+            res = BatchResult(np.zeros(m, np.uint32), np.zeros(m, np.uint64), np.zeros(m, np.uint64),
+                              np.zeros(m, np.uint64), np.zeros(m, np.uint32), None,
+                              np.zeros(m, np.uint32))
         r = GpdResult(res.status.ctypes.data, res.layers.ctypes.data, res.net_hash.ctypes.data,
                       res.tp_hash.ctypes.data, res.csum.ctypes.data, None, res.hdr_off.ctypes.data)
         n, nxt, stop = C.c_uint64(), C.c_uint64(), C.c_int()
