@@ -94,7 +94,9 @@ int gpd_pcap_index(const uint8_t *buf, uint64_t len, const gpd_pcap_info *info, 
  * directly when buf lies in memory registered with gpd_host_register), decoded, and the
  * results copied back — with two chunks in flight.  `out` holds host arrays of max_n entries
  * (status and layers required, the rest optional; ext not supported).  Returns like
- * gpd_pcap_index: the records before a rejected one are decoded and counted in *n_out. */
+ * gpd_pcap_index: the records before a rejected one are decoded and counted in *n_out.
+ * The record index (about 36 B per record) is kept per calling thread and reused by the
+ * next call, so that a replay or capture loop touches no fresh pages. */
 int gpd_decode_pcap(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, uint64_t max_n,
                     const gpd_result *out, uint64_t *n_out, uint64_t *next_pos, int *stop,
                     int nthreads);
