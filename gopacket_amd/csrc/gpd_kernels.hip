@@ -44,7 +44,8 @@ constexpr uint32_t kDiagSkipDecode = 1u << 31;  // internal diagnostic option (b
 constexpr uint32_t kDiagNoWait = 1u << 30;      // internal diagnostic: skip the per-tile DMA wait
 constexpr uint32_t kDiagNtLoad = 1u << 29;      // A/B: window LDS-DMA with the nt cache policy
 constexpr uint32_t kDiagNtStore = 1u << 28;     // A/B: result stores with the nt cache policy
-constexpr uint32_t kDiagMask = kDiagSkipDecode | kDiagNoWait | kDiagNtLoad | kDiagNtStore;
+constexpr uint32_t kShiftWindows = 1u << 27;    // internal: register-staged windows copied shifted
+constexpr uint32_t kDiagMask = kDiagSkipDecode | kDiagNoWait | kDiagNtLoad | kDiagNtStore | kShiftWindows;
 
 extern __shared__ __attribute__((aligned(16))) uint8_t g_lds[];
 
@@ -1058,6 +1059,7 @@ __device__ __forceinline__ void store_out(const KParams &P, uint32_t i, const Ou
 // A window of the batch buffer: bytes [base, base + nbytes) (base 16-aligned).
 struct Window {
   uint32_t base, nbytes;
+  uint32_t shift;  // rs_kernel: LDS byte of global byte x is buf + shift + (x - base)
 };
 
 // A window starts at the first pending packet (rounded down to 16) and covers every pending
@@ -1065,11 +1067,16 @@ struct Window {
 // the last covered lane's end is the extent; a full wave maximum only runs when some lane
 // proves otherwise.
 template <int STAGE>
-__device__ __forceinline__ Window plan_window(bool pending, uint32_t off, uint32_t end) {
-  Window w{0, 0};
+__device__ __forceinline__ Window plan_window(bool pending, uint32_t off, uint32_t end, uint32_t l3m = 14u) {
+  Window w{0, 0, 0};
   const uint64_t m = __ballot(pending);
   if (m == 0) return w;
-  w.base = __builtin_amdgcn_readlane(off, (int)__builtin_ctzll(m)) & ~15u;
+  const uint32_t first = __builtin_amdgcn_readlane(off, (int)__builtin_ctzll(m));
+  w.base = first & ~15u;
+  // the shift that puts the first packet's byte l3m (mod 16: where the wave's last network
+  // header sat, 14 for an untagged frame) on a 16-byte LDS boundary: misaligned DS reads
+  // cost ~3.6x aligned ones (tools/micro/lds_align)
+  w.shift = (32u - ((first & 15u) + l3m)) & 15u;
   const bool in = pending && off >= w.base && end - w.base <= (uint32_t)STAGE;
   const uint32_t x = in ? end - w.base : 0u;
   const uint64_t mi = __ballot(in);  // nonzero: the first pending lane is in
@@ -1274,7 +1281,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void decode_kernel(KParams P) {
     }
     PH_MARK(0);  // waiting for the window
     // ---- plan and issue the next window
-    Window Wn{0, 0};
+    Window Wn{0, 0, 0};
     uint32_t cov_n = 0;
     bool has_next = false, new_tile = false;
     if (__any(pend_p != 0)) {  // more of the planner's tile
@@ -1378,7 +1385,42 @@ typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
 // LDS bytes per wave of rs_kernel: one window (the next one waits in VGPRs), plus the chunk
 // prefix sums of the cooperative checksum for windows of 8 KiB and more.
 __host__ __device__ constexpr uint32_t rs_wave_lds_bytes(int stage) {
-  return (uint32_t)stage + (stage >= 8192 ? (uint32_t)stage / 4u + 16u : 0u);
+  return (uint32_t)stage + 16u + (stage >= 8192 ? (uint32_t)stage / 4u + 16u : 0u);
+}
+
+// Copy a register-staged window into LDS shifted up by s = 16 - 4Q - r bytes (0 < s < 16),
+// with aligned ds_write_b128 only: LDS chunk m holds bytes [16m - s, 16m - s + 16) of the
+// window, i.e. bytes [16 - s, 32 - s) of (chunk m-1 | chunk m).  Chunk m-1 of lane l is lane
+// l-1's chunk (DPP wave_shr:1), lane 0 takes lane 63's of the previous 1-KiB row; one extra
+// chunk past the window's end takes the last row's tail.
+template <int Q, int NC, typename V>
+__device__ __forceinline__ void commit_shifted(const V (&wv)[NC], uint32_t buf, uint32_t lane, uint32_t r) {
+  uint32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0;  // lane 63's chunk of the previous row
+#pragma unroll
+  for (int j = 0; j <= NC; j++) {
+    uint32_t D[8];
+    if (j < NC) {
+      D[4] = wv[j].x; D[5] = wv[j].y; D[6] = wv[j].z; D[7] = wv[j].w;
+    } else {
+      D[4] = D[5] = D[6] = D[7] = 0u;
+    }
+    D[0] = (uint32_t)__builtin_amdgcn_update_dpp((int)b0, (int)D[4], 0x138, 0xF, 0xF, false);
+    D[1] = (uint32_t)__builtin_amdgcn_update_dpp((int)b1, (int)D[5], 0x138, 0xF, 0xF, false);
+    D[2] = (uint32_t)__builtin_amdgcn_update_dpp((int)b2, (int)D[6], 0x138, 0xF, 0xF, false);
+    D[3] = (uint32_t)__builtin_amdgcn_update_dpp((int)b3, (int)D[7], 0x138, 0xF, 0xF, false);
+    V out;
+    out.x = __builtin_amdgcn_alignbyte(D[Q + 1], D[Q], r);
+    out.y = __builtin_amdgcn_alignbyte(D[Q + 2], D[Q + 1], r);
+    out.z = __builtin_amdgcn_alignbyte(D[Q + 3], D[Q + 2], r);
+    out.w = __builtin_amdgcn_alignbyte(D[Q + 4], D[Q + 3], r);
+    if (j < NC || lane == 0u) *reinterpret_cast<V *>(g_lds + buf + 1024u * j + 16u * lane) = out;
+    if (j < NC) {
+      b0 = (uint32_t)__builtin_amdgcn_readlane((int)D[4], 63);
+      b1 = (uint32_t)__builtin_amdgcn_readlane((int)D[5], 63);
+      b2 = (uint32_t)__builtin_amdgcn_readlane((int)D[6], 63);
+      b3 = (uint32_t)__builtin_amdgcn_readlane((int)D[7], 63);
+    }
+  }
 }
 
 // The fast path's streaming loop with the window staged through registers: a window's bytes
@@ -1405,7 +1447,7 @@ __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
   __syncthreads();
   const uint32_t img = (P.image_words * 4u + 15u) & ~15u;
   const uint32_t buf = img + wave * rs_wave_lds_bytes(STAGE);
-  const uint32_t pfx = buf + STAGE;
+  const uint32_t pfx = buf + STAGE + 16u;
   const uint32_t n = (uint32_t)P.n;
   const uint32_t ntiles = (n + 63u) >> 6;
   const uint32_t nwaves = gridDim.x * WAVES;
@@ -1450,10 +1492,25 @@ __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
     }
     __builtin_amdgcn_sched_barrier(0);  // issue them here, ahead of the decode
   };
-  auto wcommit = [&](const Window &) {
+  // Shifted copies pay for themselves where windows hold many small frames; the host sets
+  // the bit from the batch's mean slot (measured: tools/ab_shift.sh).
+  const bool noshift = (P.options & kShiftWindows) == 0;
+  auto wshift = [&](const Window &w) -> uint32_t { return noshift ? 0u : w.shift; };
+  auto wcommit = [&](const Window &w) {
+    const uint32_t sh = wshift(w);
+    if (sh == 0u) {
 #pragma unroll
-    for (int j = 0; j < NC; j++)
-      *reinterpret_cast<v4u32 *>(g_lds + buf + 1024u * j + 16u * lane) = wv[j];
+      for (int j = 0; j < NC; j++)
+        *reinterpret_cast<v4u32 *>(g_lds + buf + 1024u * j + 16u * lane) = wv[j];
+      return;
+    }
+    const uint32_t o = 16u - sh, r = o & 3u;
+    switch (o >> 2) {
+      case 0: commit_shifted<0, NC>(wv, buf, lane, r); break;
+      case 1: commit_shifted<1, NC>(wv, buf, lane, r); break;
+      case 2: commit_shifted<2, NC>(wv, buf, lane, r); break;
+      default: commit_shifted<3, NC>(wv, buf, lane, r); break;
+    }
   };
 
   // prologue: this tile's descriptors (waited for), the next two tiles' in flight
@@ -1467,7 +1524,8 @@ __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
   }
   uint32_t valid_p = tp * 64u + lane < n ? 1u : 0u;
   uint32_t pend_p = (valid_p && end_p - off_p <= fits) ? 1u : 0u;
-  Window Wd = plan_window<STAGE>(pend_p != 0, off_p, end_p);
+  uint32_t l3m = 14u;  // network header offset mod 16 the window shift aims at (learned)
+  Window Wd = plan_window<STAGE>(pend_p != 0, off_p, end_p, l3m);
   uint32_t cov_d = covered(Wd, pend_p, off_p, end_p);
   pend_p &= cov_d ^ 1u;
   wload(Wd);
@@ -1489,7 +1547,7 @@ __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
     wcommit(Wd);  // window k: registers -> LDS (the compiler waits for its loads here)
     PH_MARK(0);  // waiting for the window (and copying it)
     // ---- plan the next window (the next tile's descriptors landed long ago)
-    Window Wn{0, 0};
+    Window Wn{0, 0, 0};
     uint32_t cov_n = 0;
     bool has_next = false, new_tile = false;
     if (__any(pend_p != 0)) {  // more of the planner's tile
@@ -1510,7 +1568,7 @@ __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
     }
     if (new_tile) dload(tp + 2u * nwaves, o_b, c_b);
     if (has_next) {
-      Wn = plan_window<STAGE>(pend_p != 0, off_p, end_p);
+      Wn = plan_window<STAGE>(pend_p != 0, off_p, end_p, l3m);
       cov_n = covered(Wn, pend_p, off_p, end_p);
       pend_p &= cov_n ^ 1u;
       wload(Wn);
@@ -1523,7 +1581,13 @@ __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
     if (cov_d && (P.options & kDiagSkipDecode)) {  // diagnostics: data movement only
       res = Out{g_lds[buf + ((off_d - Wd.base) & ~15u)], 0, 0, 0, 0, 0};
     } else if (cov_d) {
-      if (!fast_decode<CS, HASH, COOP>(buf + (off_d - Wd.base), end_d - off_d, F, res, buf, sg)) fb = 1;
+      if (!fast_decode<CS, HASH, COOP>(buf + wshift(Wd) + (off_d - Wd.base), end_d - off_d, F, res, buf, sg))
+        fb = 1;
+    }
+    {  // learn where this wave's network headers sit (mod 16) for the next windows' shift
+      const uint32_t no = res.hoff & 0xFFFFu;
+      const uint64_t hm = __ballot(cov_d && no != 0xFFFFu);
+      if (hm) l3m = (uint32_t)__builtin_amdgcn_readlane((int)no, (int)__builtin_ctzll(hm)) & 15u;
     }
     PH_MARK(2);  // decode
     if constexpr (COOP) {  // long segments of this window: chunk prefix sums, shared

@@ -495,6 +495,16 @@ static int launch(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, hipS
      // GPD_DIAG=<0..3> overrides the two bits for A/B runs only
     static const char *d = getenv("GPD_DIAG");
     P.options |= (d ? ((uint32_t)atoi(d) & 3u) : 3u) << 28;
+    // Window copies shifted so that network headers sit 16-byte aligned in LDS, for batches
+    // of small frames (mean slot <= 96 B: a window holds 40+ packets and the saved misaligned
+    // reads outweigh the shifted copy; with IMIX-sized frames they do not).  GPD_NOSHIFT=1
+    // turns it off and GPD_SHIFT=0/1 forces it either way (A/B runs and the parity tests,
+    // which cover both copies; read per launch).
+    const char *ns = getenv("GPD_NOSHIFT");
+    const char *fs = getenv("GPD_SHIFT");
+    bool shift = mean_slot <= 96 && !(ns && atoi(ns));
+    if (fs) shift = atoi(fs) != 0;
+    if (shift) P.options |= 1u << 27;
   }
   P.nstores = 2u + (out->net_hash != nullptr) + (out->tp_hash != nullptr) + (out->csum != nullptr) +
               (out->hdr_off != nullptr);

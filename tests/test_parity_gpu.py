@@ -154,6 +154,29 @@ def test_synthetic_configs(maker):
     run_both(b, ext=False)
 
 
+@pytest.mark.parametrize("shift", ["0", "1"])
+def test_window_shift_both_ways(shift, monkeypatch):
+    """The fast kernel copies windows into LDS either as they lie or shifted so that network
+    headers land 16-byte aligned (chosen per batch by mean frame size).  Force each copy on
+    batches of every layout: aligned, packed unaligned, shuffled, pcap-like (offsets = 8 mod
+    16), tagged, VXLAN, mutated and truncated frames."""
+    monkeypatch.setenv("GPD_SHIFT", shift)
+    pk = _golden_packets()
+    run_both(PacketBatch.from_packets(pk), ext=False)
+    run_both(PacketBatch.from_packets(pk * 3, align=1), ext=False)
+    for k in (2, 8, 13):  # every start alignment class the planner's shift sees
+        b = PacketBatch.from_packets([b"\x00" * k + p for p in pk[:40]] * 2, align=16)
+        b = PacketBatch(b.data, b.data_len, (b.offset + k).astype(np.uint32), (b.caplen - k).astype(np.uint32))
+        run_both(b, ext=False)
+    mut = PacketBatch.from_packets(_mutations(seed=19, per_packet=40))
+    run_both(mut, ext=False)
+    for maker in (synth.make_udp64, synth.make_imix, synth.make_vxlan, synth.make_mixed):
+        run_both(maker(1 << 13), ext=False)
+    from gopacket_amd import pcap as NP
+    cap = NP.synth_capture(synth.make_udp64(1 << 12))
+    run_both(NP.index(cap).batch, ext=False)
+
+
 def test_layouts_unaligned_shuffled_large_empty():
     pk = _golden_packets() + [b"", b"\x01", b"\x00" * 13]
     big = [G.case_bytes(c) for c in CASES if c["name"] == "ipv6_jumbogram_dlp"][0]
