@@ -45,7 +45,9 @@ constexpr uint32_t kDiagNoWait = 1u << 30;      // internal diagnostic: skip the
 constexpr uint32_t kDiagNtLoad = 1u << 29;      // A/B: window LDS-DMA with the nt cache policy
 constexpr uint32_t kDiagNtStore = 1u << 28;     // A/B: result stores with the nt cache policy
 constexpr uint32_t kShiftWindows = 1u << 27;    // internal: register-staged windows copied shifted
-constexpr uint32_t kDiagMask = kDiagSkipDecode | kDiagNoWait | kDiagNtLoad | kDiagNtStore | kShiftWindows;
+constexpr uint32_t kRegPrefix = 1u << 26;       // internal: 8 KiB windows of long frames (IMIX)
+constexpr uint32_t kDiagMask = kDiagSkipDecode | kDiagNoWait | kDiagNtLoad | kDiagNtStore | kShiftWindows |
+                               kRegPrefix;
 
 extern __shared__ __attribute__((aligned(16))) uint8_t g_lds[];
 
@@ -1393,8 +1395,9 @@ __host__ __device__ constexpr uint32_t rs_wave_lds_bytes(int stage) {
 // window, i.e. bytes [16 - s, 32 - s) of (chunk m-1 | chunk m).  Chunk m-1 of lane l is lane
 // l-1's chunk (DPP wave_shr:1), lane 0 takes lane 63's of the previous 1-KiB row; one extra
 // chunk past the window's end takes the last row's tail.
-template <int Q, int NC, typename V>
-__device__ __forceinline__ void commit_shifted(const V (&wv)[NC], uint32_t buf, uint32_t lane, uint32_t r) {
+template <int Q, int NC, bool SUMS, typename V>
+__device__ __forceinline__ void commit_shifted(const V (&wv)[NC], uint32_t buf, uint32_t lane, uint32_t r,
+                                               uint32_t (&cs)[NC]) {
   uint32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0;  // lane 63's chunk of the previous row
 #pragma unroll
   for (int j = 0; j <= NC; j++) {
@@ -1414,6 +1417,8 @@ __device__ __forceinline__ void commit_shifted(const V (&wv)[NC], uint32_t buf, 
     out.z = __builtin_amdgcn_alignbyte(D[Q + 3], D[Q + 2], r);
     out.w = __builtin_amdgcn_alignbyte(D[Q + 4], D[Q + 3], r);
     if (j < NC || lane == 0u) *reinterpret_cast<V *>(g_lds + buf + 1024u * j + 16u * lane) = out;
+    if (SUMS && j < NC)
+      cs[j] = dot2(out.w, 0x00010001u, dot2(out.z, 0x00010001u, dot2(out.y, 0x00010001u, dot2(out.x, 0x00010001u, 0u))));
     if (j < NC) {
       b0 = (uint32_t)__builtin_amdgcn_readlane((int)D[4], 63);
       b1 = (uint32_t)__builtin_amdgcn_readlane((int)D[5], 63);
@@ -1421,6 +1426,20 @@ __device__ __forceinline__ void commit_shifted(const V (&wv)[NC], uint32_t buf, 
       b3 = (uint32_t)__builtin_amdgcn_readlane((int)D[7], 63);
     }
   }
+}
+
+// P[c] (see window_prefix) from the LE-domain sums of the chunks as committed: LDS chunk
+// 64 j + l is row j of lane l, so each row is one wave prefix scan on top of the rows below.
+template <int NC>
+__device__ __forceinline__ void rows_prefix(const uint32_t (&cs)[NC], uint32_t pfx, uint32_t lane) {
+  uint32_t base = 0;
+#pragma unroll
+  for (int j = 0; j < NC; j++) {
+    const uint32_t incl = wave_incl_scan(cs[j]);
+    *reinterpret_cast<uint32_t *>(g_lds + pfx + 4u * (64u * j + lane)) = base + incl - cs[j];
+    base += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+  }
+  if (lane == 0u) *reinterpret_cast<uint32_t *>(g_lds + pfx + 4u * 64u * NC) = base;
 }
 
 // The fast path's streaming loop with the window staged through registers: a window's bytes
@@ -1435,7 +1454,7 @@ __device__ __forceinline__ void commit_shifted(const V (&wv)[NC], uint32_t buf, 
 // window finished (deferred one iteration, so that after the next window's loads nothing else
 // is issued and the wait at the next commit covers exactly those loads)  ->  plan and load
 // window k+1  ->  decode window k from LDS.
-template <int STAGE, bool CS, bool HASH, int MINW, bool DEFER = false>
+template <int STAGE, bool CS, bool HASH, int MINW, bool DEFER = false, bool RPFX = true>
 __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
   constexpr int WAVES = 4;
   constexpr int NC = STAGE / 1024;              // 16-byte chunks per lane per window
@@ -1496,20 +1515,38 @@ __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
   // the bit from the batch's mean slot (measured: tools/ab_shift.sh).
   const bool noshift = (P.options & kShiftWindows) == 0;
   auto wshift = [&](const Window &w) -> uint32_t { return noshift ? 0u : w.shift; };
+  // COOP: the chunk prefix sums of a window are computed from the registers as it is
+  // committed when the wave's previous window needed them (`pfx_pred`); otherwise, if this
+  // window turns out to need them, window_prefix reads them back from LDS.
+  bool pfx_pred = COOP, pfx_done = false;
   auto wcommit = [&](const Window &w) {
     const uint32_t sh = wshift(w);
+    uint32_t cs[NC];
+    pfx_done = false;
+    const bool sums = COOP && RPFX && pfx_pred && sh == 0u;
     if (sh == 0u) {
 #pragma unroll
       for (int j = 0; j < NC; j++)
         *reinterpret_cast<v4u32 *>(g_lds + buf + 1024u * j + 16u * lane) = wv[j];
-      return;
+      if (sums) {
+#pragma unroll
+        for (int j = 0; j < NC; j++)
+          cs[j] = dot2(wv[j].w, 0x00010001u, dot2(wv[j].z, 0x00010001u,
+                       dot2(wv[j].y, 0x00010001u, dot2(wv[j].x, 0x00010001u, 0u))));
+      }
+    } else {
+      // (shifted windows leave the prefix to window_prefix: measured, pcap64 +2 % otherwise)
+      const uint32_t o = 16u - sh, r = o & 3u;
+      switch (o >> 2) {
+        case 0: commit_shifted<0, NC, false>(wv, buf, lane, r, cs); break;
+        case 1: commit_shifted<1, NC, false>(wv, buf, lane, r, cs); break;
+        case 2: commit_shifted<2, NC, false>(wv, buf, lane, r, cs); break;
+        default: commit_shifted<3, NC, false>(wv, buf, lane, r, cs); break;
+      }
     }
-    const uint32_t o = 16u - sh, r = o & 3u;
-    switch (o >> 2) {
-      case 0: commit_shifted<0, NC>(wv, buf, lane, r); break;
-      case 1: commit_shifted<1, NC>(wv, buf, lane, r); break;
-      case 2: commit_shifted<2, NC>(wv, buf, lane, r); break;
-      default: commit_shifted<3, NC>(wv, buf, lane, r); break;
+    if (sums) {
+      rows_prefix<NC>(cs, pfx, lane);
+      pfx_done = true;
     }
   };
 
@@ -1591,8 +1628,9 @@ __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
     }
     PH_MARK(2);  // decode
     if constexpr (COOP) {  // long segments of this window: chunk prefix sums, shared
-      if (__any(sg.b > sg.a)) {
-        window_prefix<STAGE>(buf, pfx, lane);
+      pfx_pred = __any(sg.b > sg.a);
+      if (pfx_pred) {
+        if (!pfx_done) window_prefix<STAGE>(buf, pfx, lane);
         if (sg.b > sg.a) {
           const uint32_t mid = lds_u32(pfx + 4u * sg.b) - lds_u32(pfx + 4u * sg.a);
           res.csum |= fold_le_not(sg.part + mid) << 16;
@@ -1690,7 +1728,7 @@ static int geom() {
   return g;
 }
 
-template <int STAGE, bool CS, bool HASH, int MINW, bool DEFER = false>
+template <int STAGE, bool CS, bool HASH, int MINW, bool DEFER = false, bool RPFX = true>
 static hipError_t launch_rs(const KParams &P, hipStream_t stream, int num_cus) {
   const uint64_t ntiles = (P.n + 63) / 64;
   const size_t lds = ((P.image_words * 4u + 15u) & ~15u) + 4 * (size_t)rs_wave_lds_bytes(STAGE) + 64;
@@ -1700,7 +1738,7 @@ static hipError_t launch_rs(const KParams &P, hipStream_t stream, int num_cus) {
   const uint64_t cap = (uint64_t)num_cus * per_cu * (rounds > 0 ? rounds : 4);  // rounds of resident workgroups
   if (blocks > cap) blocks = cap;
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL((rs_kernel<STAGE, CS, HASH, MINW, DEFER>), dim3((unsigned)blocks), dim3(256), lds, stream, P);
+  hipLaunchKernelGGL((rs_kernel<STAGE, CS, HASH, MINW, DEFER, RPFX>), dim3((unsigned)blocks), dim3(256), lds, stream, P);
   return hipGetLastError();
 }
 
@@ -1735,7 +1773,10 @@ static hipError_t launch_fast(const KParams &P, hipStream_t stream, int num_cus)
     return launch_rs<4096, CS, HASH, 4>(P, stream, num_cus);
   }
   if (w == 2) return launch_rs<8192, CS, HASH, 2>(P, stream, num_cus);
-  return launch_rs<8192, CS, HASH, 3>(P, stream, num_cus);
+  // The register-computed chunk prefix pays off for long frames only (IMIX -3 %); with small
+  // frames (pcap records, VXLAN) its extra registers and code cost 1-2 %.
+  if (P.options & kRegPrefix) return launch_rs<8192, CS, HASH, 3>(P, stream, num_cus);
+  return launch_rs<8192, CS, HASH, 3, false, false>(P, stream, num_cus);
 }
 
 template <bool EXT, bool PAGES>

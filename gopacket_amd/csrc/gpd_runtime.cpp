@@ -484,8 +484,8 @@ static int launch(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, hipS
   // LDS window per buffer: the smallest of 4/8 KiB that holds a typical 64-packet tile
   const uint64_t mean_slot = (in->data_len + in->n - 1) / in->n;
   P.stage = mean_slot * 64 <= 4096 ? 4096u : 8192u;
-  {  // A/B only: force the window size
-    static const char *st = getenv("GPD_STAGE");
+  {  // A/B and tests only: force the window size (read per launch)
+    const char *st = getenv("GPD_STAGE");
     if (st) P.stage = atoi(st) == 8192 ? 8192u : 4096u;
   }
   P.first = ctx->first;
@@ -505,6 +505,10 @@ static int launch(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, hipS
     bool shift = mean_slot <= 96 && !(ns && atoi(ns));
     if (fs) shift = atoi(fs) != 0;
     if (shift) P.options |= 1u << 27;
+    // long frames (mean slot > 160 B): 8 KiB windows whose chunk prefix sums are computed
+    // from the registers at commit (GPD_RPFX=0/1 forces it for A/B runs and the tests)
+    const char *rp = getenv("GPD_RPFX");
+    if (rp ? atoi(rp) != 0 : (mean_slot > 160 && !shift)) P.options |= 1u << 26;
   }
   P.nstores = 2u + (out->net_hash != nullptr) + (out->tp_hash != nullptr) + (out->csum != nullptr) +
               (out->hdr_off != nullptr);

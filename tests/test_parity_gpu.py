@@ -154,6 +154,19 @@ def test_synthetic_configs(maker):
     run_both(b, ext=False)
 
 
+@pytest.mark.parametrize("rpfx", ["0", "1"])
+def test_register_prefix_both_ways(rpfx, monkeypatch):
+    """8 KiB windows sum their chunks for long transport segments either from LDS after the
+    decode (window_prefix) or from the registers as they are committed (predicted per wave).
+    Force each on long-frame and mixed batches."""
+    monkeypatch.setenv("GPD_RPFX", rpfx)
+    monkeypatch.setenv("GPD_STAGE", "8192")
+    for maker in (synth.make_imix, synth.make_mixed, synth.make_vxlan):
+        run_both(maker(1 << 13), ext=False)
+    run_both(PacketBatch.from_packets(_mutations(seed=23, per_packet=40)), ext=False)
+    run_both(PacketBatch.from_packets(_golden_packets() * 4, align=1), ext=False)
+
+
 @pytest.mark.parametrize("shift", ["0", "1"])
 def test_window_shift_both_ways(shift, monkeypatch):
     """The fast kernel copies windows into LDS either as they lie or shifted so that network
