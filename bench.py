@@ -179,6 +179,30 @@ def bench_flows(parser, dev_batch, n, args, stream, local):
            "insert_Mpackets_per_s": round(n / ms / 1e3, 1), "reset_ms": round(float(np.mean(rst)), 4),
            "capacity": st["capacity"], "flows": st["flows"], "keyed_packets": st["packets"],
            "collisions": st["collisions"], "full": st["full"]}
+    # bursts: the same packets, each repeated 16 times back to back (descriptors only, the
+    # bytes are shared), so a wave's lanes fold 16-packet runs before their atomics
+    rep = 16
+    bb = P.DeviceBatch.__new__(P.DeviceBatch)
+    bb.n, bb.data_len, bb.data, bb.device = n, dev_batch.data_len, dev_batch.data, local
+    bb.offset = dev_batch.offset[: n // rep].repeat_interleave(rep).contiguous()
+    bb.caplen = dev_batch.caplen[: n // rep].repeat_interleave(rep).contiguous()
+    bres = P.DeviceResult(n, local, ext=False, hdr_off=True)
+    parser.decode_device(bb, bres, stream)
+    bins = []
+    for k in range(steps + 1):
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ft.Reset(stream)
+        e[0].record(stream)
+        ft.Insert(bb, bres, fid, 0, stream)
+        e[1].record(stream)
+        torch.cuda.synchronize(local)
+        if k:
+            bins.append(e[0].elapsed_time(e[1]))
+    bst = ft.Stats(stream)
+    bms = float(np.mean(bins))
+    out["bursts16"] = {"insert_ms": round(bms, 4), "insert_Mpackets_per_s": round(n / bms / 1e3, 1),
+                       "flows": bst["flows"], "keyed_packets": bst["packets"],
+                       "collisions": bst["collisions"]}
     # the flow-affine sharded table (one table per rank, key records exchanged all-to-all):
     # host clock per phase, synchronised; with one rank the exchange is skipped
     sft = FL.ShardedFlowTable(parser, cap)

@@ -101,10 +101,45 @@ __device__ __forceinline__ uint64_t fingerprint(const uint32_t (&k)[10]) {
   return h ? h : 1ull;
 }
 
-__device__ __forceinline__ void wave_count(unsigned long long *ctr, bool pred) {
-  const uint64_t m = __ballot(pred);
-  if (m && (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(m))
-    atomicAdd(ctr, (unsigned long long)__popcll(m));
+// Run counters: every lane tallies its wave's count (the ballot is wave-uniform) across the
+// grid-stride loop, and lane 0 adds the tally once when the wave ends.  One atomic per wave
+// iteration on these few shared words serialised at the memory side and cost most of the
+// insert (7.6 ms of 2^24 packets); one per wave per launch costs nothing.
+__device__ __forceinline__ void wave_tally(unsigned long long &t, bool pred) {
+  t += (unsigned long long)__popcll(__ballot(pred));
+}
+__device__ __forceinline__ void wave_flush(unsigned long long *ctr, unsigned long long t) {
+  if (t && (threadIdx.x & 63u) == 0u) atomicAdd(ctr, t);
+}
+
+// Consecutive lanes of a wave that update the same record (a burst of one flow: capture
+// order keeps a flow's packets together, and key records stay in packet order) fold their
+// updates before the atomics.  A segmented inclusive scan over runs of equal slots leaves the
+// run's min/max seq and its packet and byte sums in the run's last lane, which alone issues
+// the four atomics.  min, max and + are associative and commutative, so every record ends
+// bit-identical to one atomic per packet.  A wave with no runs (every lane a different
+// record, e.g. all new flows) skips the scan.  Called by all 64 lanes.
+// pb packs packets (bits 57-63, at most 64) and bytes (at most 64 x 2^32 < 2^57).
+constexpr int kPktShift = 57;
+__device__ __forceinline__ bool fold_run(bool counted, uint64_t s, uint64_t &mn, uint64_t &mx,
+                                         uint64_t &pb) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t key = counted ? s : ~(uint64_t)lane;  // uncounted lanes never join a run
+  const uint64_t prev = __shfl_up(key, 1u, 64);
+  const uint64_t heads = __ballot(lane == 0u || prev != key);
+  const bool tail = lane == 63u || ((heads >> (lane + 1u)) & 1ull);
+  if (heads == ~0ull) return tail;  // no two neighbours share a record
+  const uint32_t start = 63u - (uint32_t)__builtin_clzll(heads & ((2ull << lane) - 1ull));
+#pragma unroll
+  for (uint32_t d = 1; d < 64u; d <<= 1) {
+    const uint64_t omn = __shfl_up(mn, d, 64), omx = __shfl_up(mx, d, 64), opb = __shfl_up(pb, d, 64);
+    if (lane >= start + d) {
+      mn = min(mn, omn);
+      mx = max(mx, omx);
+      pb += opb;
+    }
+  }
+  return tail;
 }
 
 // Key of item i: gathered from the packet bytes, or read from a key record (KEYS).
@@ -127,6 +162,7 @@ __device__ __forceinline__ bool item_key(const FlowParams &P, uint64_t i, uint32
 
 template <bool KEYS>
 __global__ __launch_bounds__(kFlowThreads) void flow_insert_kernel(FlowParams P) {
+  unsigned long long t_flows = 0, t_packets = 0, t_nokey = 0, t_full = 0;
   for (uint64_t i = blockIdx.x * (uint64_t)kFlowThreads + threadIdx.x; i - threadIdx.x < P.n;
        i += (uint64_t)gridDim.x * kFlowThreads) {
     const bool live = i < P.n;
@@ -136,8 +172,15 @@ __global__ __launch_bounds__(kFlowThreads) void flow_insert_kernel(FlowParams P)
     const bool keyed = live && item_key<KEYS>(P, i, k, seq, caplen);
     bool created = false, full = false;
     uint64_t s = 0;
-    if (keyed) {
-      const uint64_t fp = fingerprint(k);
+    // A lane whose left neighbour holds the same fingerprint (a burst) follows the same
+    // probe sequence to the same record: only the first lane of each such run probes, and
+    // the others take its slot afterwards.
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t fp = keyed ? fingerprint(k) : 0ull;  // fingerprints are never 0
+    const uint64_t fp_prev = __shfl_up(fp, 1u, 64);
+    const uint64_t lead = __ballot(!keyed || lane == 0u || fp_prev != fp);
+    const bool probes = keyed && ((lead >> lane) & 1ull);
+    if (probes) {
       s = fp & P.mask;
       uint64_t probe = 0;
       for (; probe <= P.mask; probe++) {  // every lane leaves after at most capacity probes
@@ -159,25 +202,42 @@ __global__ __launch_bounds__(kFlowThreads) void flow_insert_kernel(FlowParams P)
       }
       if (probe > P.mask) full = true;
     }
+    if (lead != ~0ull) {  // run members take the slot their run's first lane found
+      const uint32_t start = 63u - (uint32_t)__builtin_clzll(lead & ((2ull << lane) - 1ull));
+      const uint64_t hs = __shfl(s, (int)start, 64);
+      const bool hfull = __shfl((int)full, (int)start, 64) != 0;
+      if (keyed && !probes) {
+        s = hs;
+        full = hfull;
+      }
+    }
     const bool counted = keyed && !full;
-    if (counted) {
+    uint64_t mn = seq, mx = seq, pb = (1ull << kPktShift) | caplen;
+    const bool tail = fold_run(counted, s, mn, mx, pb);
+    if (counted && tail) {
       gpd_flow_rec &r = P.tab[s];
-      atomicMin(reinterpret_cast<unsigned long long *>(&r.first), (unsigned long long)seq);
-      atomicMax(reinterpret_cast<unsigned long long *>(&r.last), (unsigned long long)seq);
-      atomicAdd(reinterpret_cast<unsigned long long *>(&r.packets), 1ull);
-      atomicAdd(reinterpret_cast<unsigned long long *>(&r.bytes), (unsigned long long)caplen);
+      atomicMin(reinterpret_cast<unsigned long long *>(&r.first), (unsigned long long)mn);
+      atomicMax(reinterpret_cast<unsigned long long *>(&r.last), (unsigned long long)mx);
+      atomicAdd(reinterpret_cast<unsigned long long *>(&r.packets), (unsigned long long)(pb >> kPktShift));
+      atomicAdd(reinterpret_cast<unsigned long long *>(&r.bytes),
+                (unsigned long long)(pb & ((1ull << kPktShift) - 1ull)));
     }
     if (live) P.flow_id[i] = !keyed ? GPD_FLOW_NONE : full ? GPD_FLOW_FULL : (uint32_t)s;
-    wave_count(P.stats + FS_FLOWS, created);
-    wave_count(P.stats + FS_PACKETS, counted);
-    wave_count(P.stats + FS_NOKEY, live && !keyed);
-    wave_count(P.stats + FS_FULL, full);
+    wave_tally(t_flows, created);
+    wave_tally(t_packets, counted);
+    wave_tally(t_nokey, live && !keyed);
+    wave_tally(t_full, full);
   }
+  wave_flush(P.stats + FS_FLOWS, t_flows);
+  wave_flush(P.stats + FS_PACKETS, t_packets);
+  wave_flush(P.stats + FS_NOKEY, t_nokey);
+  wave_flush(P.stats + FS_FULL, t_full);
 }
 
 // Second pass: every item's key against its record's stored key.
 template <bool KEYS>
 __global__ __launch_bounds__(kFlowThreads) void flow_verify_kernel(FlowParams P) {
+  unsigned long long t_coll = 0;
   for (uint64_t i = blockIdx.x * (uint64_t)kFlowThreads + threadIdx.x; i - threadIdx.x < P.n;
        i += (uint64_t)gridDim.x * kFlowThreads) {
     bool bad = false;
@@ -198,8 +258,9 @@ __global__ __launch_bounds__(kFlowThreads) void flow_verify_kernel(FlowParams P)
         }
       }
     }
-    wave_count(P.stats + FS_COLL, bad);
+    wave_tally(t_coll, bad);
   }
+  wave_flush(P.stats + FS_COLL, t_coll);
 }
 
 // Owner rank of a keyed packet: the high half of the two direction-symmetric FastHashes'

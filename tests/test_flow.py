@@ -35,6 +35,19 @@ def _hot_batch(n=20000, distinct=300, seed=3):
     return PacketBatch.from_packets([pool[int(k)] for k in rng.integers(0, len(pool), n)])
 
 
+def _burst_batch(n=20000, distinct=200, seed=7):
+    """Flows in bursts: runs of 1-150 back-to-back packets of one flow (runs cross wave
+    boundaries, unkeyed frames break some), so a wave's lanes share records and the insert
+    folds each run before its atomics; a flow recurs in later bursts."""
+    rng = np.random.default_rng(seed)
+    base = synth.make_mixed(distinct)
+    pool = [base.packet(i) for i in range(base.n)]
+    out = []
+    while len(out) < n:
+        out += [pool[int(rng.integers(0, len(pool)))]] * int(rng.integers(1, 151))
+    return PacketBatch.from_packets(out[:n])
+
+
 def test_oracle_flow_keys_directional_and_pcap():
     """The restatement on the reference's own capture: test_ethernet.pcap is one TCP
     conversation, so its packets fall into exactly two directional keys."""
@@ -86,7 +99,7 @@ def _decode_dev(p, batch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind", ["golden_mut", "mixed", "hot", "imix"])
+@pytest.mark.parametrize("kind", ["golden_mut", "mixed", "hot", "imix", "burst"])
 def test_flow_table_matches_oracle(kind):
     import torch
     from gopacket_amd import flows as FL
@@ -105,6 +118,8 @@ def test_flow_table_matches_oracle(kind):
         batch = synth.make_mixed(30000)
     elif kind == "imix":
         batch = synth.make_imix(1 << 14)
+    elif kind == "burst":
+        batch = _burst_batch()
     else:
         batch = _hot_batch()
     parser = P.NewDecodingLayerParser(L.LayerTypeEthernet, *[P.DECODER_BY_NAME[k]() for k in P.DECODER_BY_NAME])
@@ -183,8 +198,10 @@ def test_flow_owner_is_direction_symmetric():
 def _global_batch():
     pool = _hot_batch(6000, 400, 6)
     mixed = synth.make_mixed(4000, seed=0x5EED0200)
+    burst = _burst_batch(4000, 100, 8)
     return PacketBatch.from_packets([pool.packet(i) for i in range(pool.n)] +
-                                    [mixed.packet(i) for i in range(mixed.n)])
+                                    [mixed.packet(i) for i in range(mixed.n)] +
+                                    [burst.packet(i) for i in range(burst.n)])
 
 
 def _shard_worker(rank, world, port, out_dir):
