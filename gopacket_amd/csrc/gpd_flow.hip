@@ -54,6 +54,9 @@ struct FlowParams {
   gpd_flow_key *kout;         // partitioned key records (gpd_flow_keys)
   unsigned long long *parts;  // [0, nparts): counts; [nparts, 2 nparts): scatter cursors
   uint32_t nparts;
+  // insert -> verify: bit l of word w set when packet 64w+l claimed its record (and so wrote
+  // the key the verify would compare against); one word per wave iteration
+  uint64_t *made = nullptr;
 };
 
 // The key of packet i as 10 words: src[16], dst[16], ports (raw wire bytes), types.  Returns
@@ -211,6 +214,8 @@ __global__ __launch_bounds__(kFlowThreads) void flow_insert_kernel(FlowParams P)
         full = hfull;
       }
     }
+    const uint64_t made = __ballot(created);
+    if (lane == 0u && i < P.n) P.made[i >> 6] = made;  // i = the wave's first packet
     const bool counted = keyed && !full;
     uint64_t mn = seq, mx = seq, pb = (1ull << kPktShift) | caplen;
     const bool tail = fold_run(counted, s, mn, mx, pb);
@@ -246,7 +251,9 @@ __global__ __launch_bounds__(kFlowThreads) void flow_verify_kernel(FlowParams P)
       uint32_t k[10];
       uint64_t seq;
       uint32_t caplen;
-      if (id < GPD_FLOW_FULL && item_key<KEYS>(P, i, k, seq, caplen)) {
+      // a packet that claimed its record wrote that record's key itself
+      const bool made = (P.made[i >> 6] >> (threadIdx.x & 63u)) & 1ull;
+      if (id < GPD_FLOW_FULL && !made && item_key<KEYS>(P, i, k, seq, caplen)) {
         const gpd_flow_rec &r = P.tab[id];
         const uint32_t *w = reinterpret_cast<const uint32_t *>(r.src);
         bool same = k[9] == ((uint32_t)r.net_type | ((uint32_t)r.tp_type << 8) | ((uint32_t)r.addr_len << 16));
@@ -427,6 +434,8 @@ struct gpd_flowtable {
   unsigned long long *stats = nullptr;  // FS_WORDS counters
   unsigned long long *parts = nullptr;  // gpd_flow_keys: nparts x grid counts (+ totals), grown on use
   uint64_t parts_words = 0;
+  uint64_t *made = nullptr;  // insert -> verify claim bits, one word per 64 packets, grown on use
+  uint64_t made_words = 0;
 };
 
 #define FLOW_TRY(expr)                                                                      \
@@ -439,6 +448,20 @@ struct gpd_flowtable {
 static unsigned grid_for(uint64_t work, int num_cus) {
   const uint64_t blocks = (work + gpd::kFlowThreads - 1) / gpd::kFlowThreads;
   return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)num_cus * 8));
+}
+
+static hipError_t grow_made(gpd_flowtable *ft, uint64_t n) {
+  const uint64_t words = (n + 63) / 64;
+  if (ft->made_words >= words) return hipSuccess;
+  if (ft->made) {
+    const hipError_t e = hipFree(ft->made);
+    if (e != hipSuccess) return e;
+  }
+  ft->made = nullptr;
+  ft->made_words = 0;
+  const hipError_t e = hipMalloc(&ft->made, words * sizeof(uint64_t));
+  if (e == hipSuccess) ft->made_words = words;
+  return e;
 }
 
 extern "C" {
@@ -497,6 +520,8 @@ int gpd_flow_insert(gpd_flowtable *ft, const gpd_batch *in, const gpd_result *re
   gpd::FlowParams P{in->data, in->data_len, in->offset, in->caplen, res->status, res->hdr_off,
                     flow_id, in->n, index_base, ft->tab, ft->cap - 1, ft->stats,
                     nullptr, nullptr, nullptr, nullptr, nullptr, 0};
+  FLOW_TRY(grow_made(ft, in->n));
+  P.made = ft->made;
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid(grid_for(in->n, ft->num_cus)), block(gpd::kFlowThreads);
   hipLaunchKernelGGL(gpd::flow_insert_kernel<false>, grid, block, 0, s, P);
@@ -574,6 +599,8 @@ int gpd_flow_insert_keys(gpd_flowtable *ft, const gpd_flow_key *keys, uint64_t n
   FLOW_TRY(hipSetDevice(ft->device));
   gpd::FlowParams P{nullptr, 0, nullptr, nullptr, nullptr, nullptr, flow_id, n, 0, ft->tab,
                     ft->cap - 1, ft->stats, keys, nullptr, nullptr, nullptr, nullptr, 0};
+  FLOW_TRY(grow_made(ft, n));
+  P.made = ft->made;
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid(grid_for(n, ft->num_cus)), block(gpd::kFlowThreads);
   hipLaunchKernelGGL(gpd::flow_insert_kernel<true>, grid, block, 0, s, P);
@@ -646,6 +673,7 @@ int gpd_flow_destroy(gpd_flowtable *ft) {
   if (ft->tab) (void)hipFree(ft->tab);
   if (ft->stats) (void)hipFree(ft->stats);
   if (ft->parts) (void)hipFree(ft->parts);
+  if (ft->made) (void)hipFree(ft->made);
   delete ft;
   return GPD_OK;
 }
