@@ -14,9 +14,11 @@
 // straight from the packet bytes in HBM: 16+16 address bytes, 4 port bytes, the types.
 // Records live in an open-addressing table of 2^k 80-byte records.  A record is claimed by
 // one 64-bit compare-and-swap of the key's fingerprint; the claimer then stores the key.
-// The per-flow counters are device atomics.  A second launch compares every packet's key
-// with its record's stored key (visible after the launch boundary), so a fingerprint
-// collision is caught and reported instead of silently merging two flows.
+// The per-flow counters are device atomics, folded first over runs of neighbouring lanes on
+// one record (fold_run).  A second launch compares every packet's key with its record's
+// stored key (visible after the launch boundary), so a fingerprint collision is caught and
+// reported instead of silently merging two flows; packets that claimed their record wrote
+// its key themselves and are skipped (the insert's claim bits, FlowParams::made).
 // Sharding over GPUs (gpd_flow_keys / gpd_flow_insert_keys): the same key, gathered once,
 // travels as a 64-byte record to the rank its FastHash pair names; two passes (count per
 // owner, then scatter with wave-aggregated cursors) group the records by owner without a
