@@ -127,14 +127,15 @@ __device__ __forceinline__ void wave_flush(unsigned long long *ctr, unsigned lon
 // pb packs packets (bits 57-63, at most 64) and bytes (at most 64 x 2^32 < 2^57).
 constexpr int kPktShift = 57;
 __device__ __forceinline__ bool fold_run(bool counted, uint64_t s, uint64_t &mn, uint64_t &mx,
-                                         uint64_t &pb) {
+                                         uint64_t &pb, uint32_t &start) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t key = counted ? s : ~(uint64_t)lane;  // uncounted lanes never join a run
   const uint64_t prev = __shfl_up(key, 1u, 64);
   const uint64_t heads = __ballot(lane == 0u || prev != key);
   const bool tail = lane == 63u || ((heads >> (lane + 1u)) & 1ull);
+  start = lane;
   if (heads == ~0ull) return tail;  // no two neighbours share a record
-  const uint32_t start = 63u - (uint32_t)__builtin_clzll(heads & ((2ull << lane) - 1ull));
+  start = 63u - (uint32_t)__builtin_clzll(heads & ((2ull << lane) - 1ull));
 #pragma unroll
   for (uint32_t d = 1; d < 64u; d <<= 1) {
     const uint64_t omn = __shfl_up(mn, d, 64), omx = __shfl_up(mx, d, 64), opb = __shfl_up(pb, d, 64);
@@ -145,6 +146,38 @@ __device__ __forceinline__ bool fold_run(bool counted, uint64_t s, uint64_t &mn,
     }
   }
   return tail;
+}
+
+// The counter updates of one run (fold_run's totals, in its last lane).  A run whose first
+// lane claimed the record in this launch is the record's first writer, so the insert stores
+// its totals plainly; every other run adds them with atomics in the verify launch, after
+// those stores (the launch boundary orders them).  So a new flow costs its claim CAS and
+// plain stores, and the atomics are left to packets of flows that already existed.
+__device__ __forceinline__ void store_run(gpd_flow_rec &r, uint64_t mn, uint64_t mx, uint64_t pb) {
+  r.first = mn;
+  r.last = mx;
+  r.packets = pb >> kPktShift;
+  r.bytes = pb & ((1ull << kPktShift) - 1ull);
+}
+__device__ __forceinline__ void add_run(gpd_flow_rec &r, uint64_t mn, uint64_t mx, uint64_t pb) {
+  atomicMin(reinterpret_cast<unsigned long long *>(&r.first), (unsigned long long)mn);
+  atomicMax(reinterpret_cast<unsigned long long *>(&r.last), (unsigned long long)mx);
+  atomicAdd(reinterpret_cast<unsigned long long *>(&r.packets), (unsigned long long)(pb >> kPktShift));
+  atomicAdd(reinterpret_cast<unsigned long long *>(&r.bytes),
+            (unsigned long long)(pb & ((1ull << kPktShift) - 1ull)));
+}
+
+// Sequence number and captured length of item i.
+template <bool KEYS>
+__device__ __forceinline__ void item_seq(const FlowParams &P, uint64_t i, uint64_t &seq,
+                                         uint32_t &caplen) {
+  if constexpr (KEYS) {
+    seq = P.keys[i].seq;
+    caplen = P.keys[i].caplen;
+  } else {
+    seq = P.base + i;
+    caplen = P.caplen[i];
+  }
 }
 
 // Key of item i: gathered from the packet bytes, or read from a key record (KEYS).
@@ -220,15 +253,9 @@ __global__ __launch_bounds__(kFlowThreads) void flow_insert_kernel(FlowParams P)
     if (lane == 0u && i < P.n) P.made[i >> 6] = made;  // i = the wave's first packet
     const bool counted = keyed && !full;
     uint64_t mn = seq, mx = seq, pb = (1ull << kPktShift) | caplen;
-    const bool tail = fold_run(counted, s, mn, mx, pb);
-    if (counted && tail) {
-      gpd_flow_rec &r = P.tab[s];
-      atomicMin(reinterpret_cast<unsigned long long *>(&r.first), (unsigned long long)mn);
-      atomicMax(reinterpret_cast<unsigned long long *>(&r.last), (unsigned long long)mx);
-      atomicAdd(reinterpret_cast<unsigned long long *>(&r.packets), (unsigned long long)(pb >> kPktShift));
-      atomicAdd(reinterpret_cast<unsigned long long *>(&r.bytes),
-                (unsigned long long)(pb & ((1ull << kPktShift) - 1ull)));
-    }
+    uint32_t start;
+    const bool tail = fold_run(counted, s, mn, mx, pb, start);
+    if (counted && tail && ((made >> start) & 1ull)) store_run(P.tab[s], mn, mx, pb);
     if (live) P.flow_id[i] = !keyed ? GPD_FLOW_NONE : full ? GPD_FLOW_FULL : (uint32_t)s;
     wave_tally(t_flows, created);
     wave_tally(t_packets, counted);
@@ -241,21 +268,34 @@ __global__ __launch_bounds__(kFlowThreads) void flow_insert_kernel(FlowParams P)
   wave_flush(P.stats + FS_FULL, t_full);
 }
 
-// Second pass: every item's key against its record's stored key.
+// Second pass: the counter updates of runs that found an existing record, and every item's
+// key against its record's stored key.
 template <bool KEYS>
 __global__ __launch_bounds__(kFlowThreads) void flow_verify_kernel(FlowParams P) {
   unsigned long long t_coll = 0;
   for (uint64_t i = blockIdx.x * (uint64_t)kFlowThreads + threadIdx.x; i - threadIdx.x < P.n;
        i += (uint64_t)gridDim.x * kFlowThreads) {
     bool bad = false;
+    // the insert's runs again (same lanes, same slots); a run whose first lane claimed the
+    // record has stored its totals already
+    const uint32_t id = i < P.n ? P.flow_id[i] : GPD_FLOW_NONE;
+    const uint64_t made = i - (threadIdx.x & 63u) < P.n ? P.made[i >> 6] : 0ull;
+    const bool counted = id < GPD_FLOW_FULL;
+    uint64_t mn = 0, mx = 0, pb = 0;
+    uint32_t caplen = 0, start;
+    if (counted && !((made >> (threadIdx.x & 63u)) & 1ull)) {
+      item_seq<KEYS>(P, i, mn, caplen);
+      mx = mn;
+      pb = (1ull << kPktShift) | caplen;
+    }
+    const bool tail = fold_run(counted, id, mn, mx, pb, start);
+    if (counted && tail && !((made >> start) & 1ull)) add_run(P.tab[id], mn, mx, pb);
     if (i < P.n) {
-      const uint32_t id = P.flow_id[i];
       uint32_t k[10];
       uint64_t seq;
-      uint32_t caplen;
       // a packet that claimed its record wrote that record's key itself
-      const bool made = (P.made[i >> 6] >> (threadIdx.x & 63u)) & 1ull;
-      if (id < GPD_FLOW_FULL && !made && item_key<KEYS>(P, i, k, seq, caplen)) {
+      const bool mine = (made >> (threadIdx.x & 63u)) & 1ull;
+      if (counted && !mine && item_key<KEYS>(P, i, k, seq, caplen)) {
         const gpd_flow_rec &r = P.tab[id];
         const uint32_t *w = reinterpret_cast<const uint32_t *>(r.src);
         bool same = k[9] == ((uint32_t)r.net_type | ((uint32_t)r.tp_type << 8) | ((uint32_t)r.addr_len << 16));
