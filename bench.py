@@ -174,11 +174,24 @@ def bench_flows(parser, dev_batch, n, args, stream, local):
             rst.append(e[0].elapsed_time(e[1]))
             ins.append(e[1].elapsed_time(e[2]))
     st = ft.Stats(stream)
+    # the same packets again into the filled table: every packet finds an existing flow
+    ex = []
+    for k in range(steps):
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ft.Reset(stream)
+        ft.Insert(dev_batch, res, fid, 0, stream)
+        e[0].record(stream)
+        ft.Insert(dev_batch, res, fid, n, stream)
+        e[1].record(stream)
+        torch.cuda.synchronize(local)
+        ex.append(e[0].elapsed_time(e[1]))
     ms = float(np.mean(ins))
     out = {"diag": "F3 flow table (not the metric)", "packets": n, "insert_ms": round(ms, 4),
            "insert_Mpackets_per_s": round(n / ms / 1e3, 1), "reset_ms": round(float(np.mean(rst)), 4),
            "capacity": st["capacity"], "flows": st["flows"], "keyed_packets": st["packets"],
-           "collisions": st["collisions"], "full": st["full"]}
+           "collisions": st["collisions"], "full": st["full"],
+           "existing_flows": {"insert_ms": round(float(np.mean(ex)), 4),
+                              "insert_Mpackets_per_s": round(n / float(np.mean(ex)) / 1e3, 1)}}
     # bursts: the same packets, each repeated 16 times back to back (descriptors only, the
     # bytes are shared), so a wave's lanes fold 16-packet runs before their atomics
     rep = 16

@@ -222,8 +222,11 @@ __global__ __launch_bounds__(kFlowThreads) void flow_insert_kernel(FlowParams P)
       s = fp & P.mask;
       uint64_t probe = 0;
       for (; probe <= P.mask; probe++) {  // every lane leaves after at most capacity probes
-        const unsigned long long old =
-            atomicCAS(reinterpret_cast<unsigned long long *>(&P.tab[s].fp), 0ull, (unsigned long long)fp);
+        // a record's fingerprint only goes 0 -> fp within a launch, so a plain read that sees
+        // a fingerprint is final; only an empty slot needs the compare-and-swap
+        unsigned long long old = *reinterpret_cast<volatile unsigned long long *>(&P.tab[s].fp);
+        if (old == 0ull)
+          old = atomicCAS(reinterpret_cast<unsigned long long *>(&P.tab[s].fp), 0ull, (unsigned long long)fp);
         if (old == 0ull) {  // claimed: store the key (read by the verify launch)
           gpd_flow_rec &r = P.tab[s];
           uint32_t *w = reinterpret_cast<uint32_t *>(r.src);
