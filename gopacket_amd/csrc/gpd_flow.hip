@@ -160,7 +160,10 @@ __device__ __forceinline__ void store_run(gpd_flow_rec &r, uint64_t mn, uint64_t
   r.bytes = pb & ((1ull << kPktShift) - 1ull);
 }
 __device__ __forceinline__ void add_run(gpd_flow_rec &r, uint64_t mn, uint64_t mx, uint64_t pb) {
-  atomicMin(reinterpret_cast<unsigned long long *>(&r.first), (unsigned long long)mn);
+  // `first` only falls: a read at or below mn (a flow seen in an earlier batch) proves the
+  // min a no-op; a stale read is only ever larger, and then the atomic runs
+  const uint64_t f = *reinterpret_cast<volatile uint64_t *>(&r.first);
+  if (mn < f) atomicMin(reinterpret_cast<unsigned long long *>(&r.first), (unsigned long long)mn);
   atomicMax(reinterpret_cast<unsigned long long *>(&r.last), (unsigned long long)mx);
   atomicAdd(reinterpret_cast<unsigned long long *>(&r.packets), (unsigned long long)(pb >> kPktShift));
   atomicAdd(reinterpret_cast<unsigned long long *>(&r.bytes),
