@@ -71,9 +71,10 @@ typedef struct gpd_flow_stats {
 typedef struct gpd_flowtable gpd_flowtable;
 
 /* A table of at least `capacity` records (rounded up to a power of two) on ctx's device.
- * Like the reference's StreamPool under its mutex (tcpassembly/assembly.go:313), one table takes one call at a time: its
- * inserts share per-table scratch (claim bits, partition counts), so calls on a table must
- * be ordered on one stream (or synchronised between streams). */
+ * Like the reference's StreamPool under its mutex (tcpassembly/assembly.go:313), a table
+ * takes one call at a time: its inserts share per-table scratch (claim bits, partition
+ * counts), so calls on a table must be ordered on one stream (or synchronised between
+ * streams). */
 int gpd_flow_create(gpd_ctx *ctx, uint64_t capacity, gpd_flowtable **out);
 /* Empty the table (asynchronous on `stream`). */
 int gpd_flow_reset(gpd_flowtable *ft, void *stream);
