@@ -60,6 +60,13 @@ EXPORTS = {
     "gpd_decode_pcap": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64,
                                   C.POINTER(GpdResult), C.POINTER(C.c_uint64),
                                   C.POINTER(C.c_uint64), C.POINTER(C.c_int), C.c_int]),
+    "gpd_decode_pcap_at": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(GpdPcapInfo),
+                                     C.c_uint64, C.c_uint64, C.POINTER(GpdResult),
+                                     C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                     C.POINTER(C.c_int), C.c_int]),
+    "gpd_pcap_locate": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(GpdPcapInfo), C.c_uint64,
+                                  C.c_void_p, C.c_uint64, C.c_void_p, C.POINTER(C.c_uint64),
+                                  C.POINTER(C.c_int), C.c_int]),
     "gpd_pcap_last_stats": (None, [C.POINTER(C.c_int)] * 3),
     "gpd_host_register": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
     "gpd_host_unregister": (C.c_int, [C.c_void_p, C.c_void_p]),

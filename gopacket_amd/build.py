@@ -3,6 +3,7 @@
   gopacket_amd/libgpd.so       product: HIP kernels (gfx950) + C-ABI runtime (include/gpd.h)
   oracle/libgpd_oracle.so      test infrastructure: CPU restatement (oracle/)
   tests/c/abi_host             test driver: a plain C host on the C-ABI (no Python/torch)
+  gopacket_amd/libgpd_synth.so workload generator for the bench (config 5 captures); not product
 
 Both are built with plain compiler invocations (hipcc / gcc); no cmake.  The .so
 files are git-ignored and travel to the GPU box with the repository snapshot.
@@ -59,6 +60,17 @@ def build_oracle(force: bool = False) -> str:
 
 
 ABI_HOST = os.path.join(ROOT, "tests", "c", "abi_host")
+SYNTH_LIB = os.path.join(PKG, "libgpd_synth.so")
+
+
+def build_synth(force: bool = False) -> str:
+    """gopacket_amd/libgpd_synth.so: the native twin of synth.make_udp64 (plain C, gcc)."""
+    src = os.path.join(CSRC, "synth", "gpd_synth.c")
+    if force or _stale(SYNTH_LIB, [src]):
+        subprocess.run(["gcc", "-O2", "-std=c11", "-Wall", "-fPIC", "-shared", "-pthread", src,
+                        "-o", SYNTH_LIB + ".tmp"], check=True)
+        os.replace(SYNTH_LIB + ".tmp", SYNTH_LIB)
+    return SYNTH_LIB
 
 
 def build_abi_host(force: bool = False) -> str:
@@ -80,3 +92,4 @@ if __name__ == "__main__":
     print(build_lib(force=force, verbose=True))
     print(build_oracle(force=force))
     print(build_abi_host(force=force))
+    print(build_synth(force=force))

@@ -131,6 +131,7 @@ struct PcapSlice {
 };
 struct PcapWalk {
   std::vector<Recs> R;          // per segment, then sequential re-walks
+  size_t used = 0;              // stretches of R in use (the rest keep their allocations)
   std::vector<PcapSlice> plan;  // the walk, in order
   uint64_t n = 0, next_pos = 0;
   int stop = 0, threads = 0, met = 0, rewalks = 0;
@@ -140,6 +141,9 @@ int pcap_walk(const uint8_t *buf, uint64_t len, const gpd_pcap_info &I, uint64_t
               int nthreads, PcapWalk &W);
 void pcap_emit(const PcapWalk &W, uint64_t base, uint32_t *off32, uint64_t *pos64, uint32_t *cap,
                uint32_t *wire, uint64_t *ts);
+int pcap_locate(const uint8_t *buf, uint64_t len, const gpd_pcap_info &I, uint64_t pos,
+                const uint64_t *targets, uint64_t k, uint64_t *pos_out, uint64_t *n_total, int *stop,
+                int nthreads);
 
 // Multiplicative hash of a 16-bit key into 2^bits buckets (host and device must agree).
 __host__ __device__ inline uint32_t key_hash(uint32_t key, uint32_t mult, uint32_t bits) {

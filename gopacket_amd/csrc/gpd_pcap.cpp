@@ -134,37 +134,165 @@ thread_local int g_last_threads = 0, g_last_rewalks = 0, g_last_met = 0;
 // nthreads <= 0: the machine's cores, at most 16 (a GPU's share of a shared host)
 int default_threads() { return (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency())); }
 
+// Counting walk (gpd_pcap_locate): the same steps as walk() without storing the records; the
+// first `keep` positions are remembered so that a speculative segment can be met.
+struct Count {
+  uint64_t n = 0;
+  std::vector<uint64_t> first;
+  End e;
+};
+void count_walk(const uint8_t *buf, uint64_t len, const gpd_pcap_info &I, uint64_t p, uint64_t limit,
+                uint64_t max_n, size_t keep, Count &c) {
+  c.n = 0;
+  c.first.clear();
+  while (p < limit) {
+    if (c.n == max_n) {
+      c.e.stop = GPD_PCAP_STOP_LIMIT;
+      c.e.pos = p;
+      c.e.stopped = true;
+      return;
+    }
+    uint32_t cap, wire;
+    uint64_t ts;
+    if (!step(buf, len, I, p, cap, wire, ts, c.e)) {
+      c.e.pos = p;
+      c.e.stopped = true;
+      return;
+    }
+    if (c.first.size() < keep) c.first.push_back(p);
+    c.n++;
+    p += GPD_PCAP_RECORD_BYTES + (uint64_t)cap;
+    __builtin_prefetch(buf + std::min(p + 2048, len), 0, 0);
+    __builtin_prefetch(buf + std::min(p + 4096, len), 0, 0);
+  }
+  c.e.pos = p;
+  c.e.stopped = false;
+}
+
 }  // namespace
 
-// The sequential walk's result over buf[pos:len) (see gpd_pcap.h), built in parallel: per
-// segment record lists plus the in-order plan of slices that make up the walk.
-int pcap_walk(const uint8_t *buf, uint64_t len, const gpd_pcap_info &I, uint64_t pos, uint64_t max_n,
-              int nthreads, PcapWalk &W) {
-  for (auto &r : W.R) r.clear();  // a reused walk keeps its allocations
-  W.plan.clear();
-  W.n = W.next_pos = 0;
-  W.stop = W.threads = W.met = W.rewalks = 0;
-  W.a0 = W.a1 = 0;
+// gpd_pcap_locate (see gpd_pcap.h): one parallel counting pass over buf[pos:len) gives every
+// segment's record count on the true walk (speculation + stitching as in pcap_walk); each
+// target is then reached by a sequential walk inside the one segment that holds it.
+int pcap_locate(const uint8_t *buf, uint64_t len, const gpd_pcap_info &I, uint64_t pos,
+                const uint64_t *targets, uint64_t k, uint64_t *pos_out, uint64_t *n_total, int *stop_out,
+                int nthreads) {
   if (nthreads <= 0) nthreads = default_threads();
   const uint64_t span = len > pos ? len - pos : 0;
   const uint64_t kMinSeg = 4ull << 20;
-  int T = (int)std::min<uint64_t>((uint64_t)nthreads, std::max<uint64_t>(1, span / kMinSeg));
-  if (max_n < span / GPD_PCAP_RECORD_BYTES) T = 1;  // a bounded walk (a chunk): sequential
+  const int T = (int)std::min<uint64_t>((uint64_t)nthreads, std::max<uint64_t>(1, span / kMinSeg));
+  std::vector<uint64_t> seg(T + 1);
+  for (int s = 0; s <= T; s++) seg[s] = pos + span * (uint64_t)s / (uint64_t)T;
+  const size_t kKeep = 4096;  // a speculation that syncs later than this is re-walked
+  std::vector<Count> C(T);
+  auto run = [&](int s) {
+    if (s == 0) {
+      count_walk(buf, len, I, pos, seg[1], UINT64_MAX, 0, C[0]);
+      return;
+    }
+    const uint64_t hi = std::min<uint64_t>(seg[s + 1], seg[s] + GPD_PCAP_RECORD_BYTES + (uint64_t)I.snaplen + 1);
+    for (uint64_t x = seg[s]; x < hi; x++) {
+      if (plausible_chain(buf, len, I, x, 8)) {
+        count_walk(buf, len, I, x, seg[s + 1], UINT64_MAX, kKeep, C[s]);
+        return;
+      }
+    }
+    C[s].e.stopped = false;
+    C[s].e.pos = UINT64_MAX;
+  };
+  if (T == 1) {
+    run(0);
+  } else {
+    std::vector<std::thread> th;
+    for (int s = 1; s < T; s++) th.emplace_back(run, s);
+    run(0);
+    for (auto &t : th) t.join();
+  }
+  // stitch: the true walk's entry position and record count before each segment
+  std::vector<uint64_t> entry(T + 1, UINT64_MAX), before(T + 1, 0);
+  entry[0] = pos;
+  End cur = C[0].e;
+  uint64_t n = C[0].n;
+  int last = 0;  // the last segment the true walk enters
+  for (int s = 1; s < T && !cur.stopped; s++) {
+    entry[s] = cur.pos;
+    before[s] = n;
+    last = s;
+    if (cur.pos >= seg[s + 1]) continue;  // no true record starts in segment s
+    const auto &F = C[s].first;
+    auto it = std::lower_bound(F.begin(), F.end(), cur.pos);
+    if (it != F.end() && *it == cur.pos) {
+      n += C[s].n - (uint64_t)(it - F.begin());
+      cur = C[s].e;
+    } else {
+      Count c;
+      count_walk(buf, len, I, cur.pos, seg[s + 1], UINT64_MAX, 0, c);
+      n += c.n;
+      cur = c.e;
+    }
+  }
+  if (!cur.stopped) cur.stop = GPD_PCAP_STOP_EOF;
+  if (n_total) *n_total = n;
+  if (stop_out) *stop_out = cur.stop;
+  uint64_t at_pos = pos, at_n = 0;  // the last position resolved (targets ascend)
+  for (uint64_t t = 0; t < k; t++) {
+    const uint64_t want = targets[t];
+    if (t && want < targets[t - 1]) return set_error(GPD_ERR_INVALID, "gpd_pcap_locate: targets must ascend");
+    if (want > n) return set_error(GPD_ERR_INVALID, "gpd_pcap_locate: target %llu beyond the %llu records of the walk",
+                                   (unsigned long long)want, (unsigned long long)n);
+    if (want == n) {
+      pos_out[t] = cur.pos;
+      continue;
+    }
+    int s = last;  // start from the nearest known point before the target
+    while (s > 0 && before[s] > want) s--;
+    if (before[s] > at_n) {
+      at_n = before[s];
+      at_pos = entry[s];
+    }
+    Count c;
+    count_walk(buf, len, I, at_pos, len, want - at_n, 0, c);
+    pos_out[t] = at_pos = c.e.pos;
+    at_n = want;
+  }
+  return GPD_OK;
+}
+
+namespace {
+
+// Stretch r of the walk's record lists, cleared, its allocation kept (a reused walk touches no
+// fresh pages).
+Recs &stretch(PcapWalk &W, size_t r) {
+  if (W.R.size() <= r) W.R.resize(r + 1);
+  W.R[r].clear();
+  return W.R[r];
+}
+
+// The true walk over the window buf[pos:end) appended to W's plan: the records whose headers
+// start before `end` (at most max_n when one thread walks the window), then the exit (the
+// first record header at or past `end`) or the stop.  With T > 1 threads the window is cut
+// into T segments; every segment but the first is walked speculatively from the first
+// position whose header chain looks like pcap records, and the segments are stitched in order.
+End walk_window(const uint8_t *buf, uint64_t len, const gpd_pcap_info &I, uint64_t pos, uint64_t end,
+                uint64_t max_n, int T, PcapWalk &W) {
+  const uint64_t span = end - pos;
   std::vector<uint64_t> seg(T + 1);
   for (int k = 0; k <= T; k++) seg[k] = pos + span * (uint64_t)k / (uint64_t)T;
-  W.R.resize((size_t)T);
+  const size_t r0 = W.used;
+  for (int k = 0; k < T; k++)
+    stretch(W, r0 + k).reserve((size_t)std::min<uint64_t>((seg[k + 1] - seg[k]) / 96 + 16, max_n + 16));
+  W.used += (size_t)T;
   std::vector<End> E(T);
-  for (int k = 0; k < T; k++) W.R[k].reserve((size_t)((seg[k + 1] - seg[k]) / 96 + 16));
   auto run = [&](int k) {
     if (k == 0) {
-      walk(buf, len, I, pos, seg[1], T == 1 ? max_n : UINT64_MAX, W.R[0], E[0]);
+      walk(buf, len, I, pos, seg[1], T == 1 ? max_n : UINT64_MAX, W.R[r0], E[0]);
       return;
     }
     // speculation: the first position of the segment that starts a plausible chain
     const uint64_t hi = std::min<uint64_t>(seg[k + 1], seg[k] + GPD_PCAP_RECORD_BYTES + (uint64_t)I.snaplen + 1);
     for (uint64_t x = seg[k]; x < hi; x++) {
       if (plausible_chain(buf, len, I, x, 8)) {
-        walk(buf, len, I, x, seg[k + 1], UINT64_MAX, W.R[k], E[k]);
+        walk(buf, len, I, x, seg[k + 1], UINT64_MAX, W.R[r0 + k], E[k]);
         return;
       }
     }
@@ -180,28 +308,86 @@ int pcap_walk(const uint8_t *buf, uint64_t len, const gpd_pcap_info &I, uint64_t
     for (auto &t : th) t.join();
   }
   // stitch in order (no copies: the plan lists slices of the segment lists)
-  W.threads = T;
-  W.plan.push_back(PcapSlice{0, 0, W.R[0].size()});
+  W.threads = std::max(W.threads, T);
+  W.plan.push_back(PcapSlice{r0, 0, W.R[r0].size()});
   End cur = E[0];
   for (int k = 1; k < T && !cur.stopped; k++) {
     if (cur.pos >= seg[k + 1]) continue;  // no true record starts in segment k
-    const auto &P = W.R[k].pos;
+    const auto &P = W.R[r0 + k].pos;
     auto it = std::lower_bound(P.begin(), P.end(), cur.pos);
     if (it != P.end() && *it == cur.pos) {  // the true walk meets the speculation
       const size_t j = (size_t)(it - P.begin());
-      W.plan.push_back(PcapSlice{(size_t)k, j, P.size() - j});
+      W.plan.push_back(PcapSlice{r0 + (size_t)k, j, P.size() - j});
       cur = E[k];
       W.met++;
     } else {  // it never does: walk this segment sequentially
-      W.R.emplace_back();
+      const size_t r = W.used++;
       End e;
-      walk(buf, len, I, cur.pos, seg[k + 1], UINT64_MAX, W.R.back(), e);
-      W.plan.push_back(PcapSlice{W.R.size() - 1, 0, W.R.back().size()});
+      walk(buf, len, I, cur.pos, seg[k + 1], UINT64_MAX, stretch(W, r), e);
+      W.plan.push_back(PcapSlice{r, 0, W.R[r].size()});
       cur = e;
       W.rewalks++;
     }
   }
-  if (!cur.stopped) {  // the last segment ends at len: the next header starts exactly there
+  return cur;
+}
+
+}  // namespace
+
+// The sequential walk's result over buf[pos:len) (see gpd_pcap.h), built in parallel: per
+// segment record lists plus the in-order plan of slices that make up the walk.
+//
+// An unbounded walk is one window over the whole buffer.  A bounded one (max_n records, e.g.
+// one chunk of a replay) must not read the whole buffer, so it goes window by window: the
+// first 256 records are walked sequentially to learn the mean record size, and each window
+// spans the bytes the records still missing would take at 1.25x that mean; windows are
+// walked in parallel like the whole buffer, and the walk continues from a window's exit
+// until it has max_n records or stops.  Windows only bound how far each step reads ahead:
+// the records and the stop are the sequential walk's.
+int pcap_walk(const uint8_t *buf, uint64_t len, const gpd_pcap_info &I, uint64_t pos, uint64_t max_n,
+              int nthreads, PcapWalk &W) {
+  W.used = 0;
+  W.plan.clear();
+  W.n = W.next_pos = 0;
+  W.stop = W.threads = W.met = W.rewalks = 0;
+  W.a0 = W.a1 = 0;
+  if (nthreads <= 0) nthreads = default_threads();
+  const uint64_t kMinSeg = 4ull << 20;
+  auto threads_for = [&](uint64_t span) {
+    return (int)std::min<uint64_t>((uint64_t)nthreads, std::max<uint64_t>(1, span / kMinSeg));
+  };
+  const uint64_t span = len > pos ? len - pos : 0;
+  End cur;
+  uint64_t have = 0;  // records in the plan
+  if (max_n >= span / GPD_PCAP_RECORD_BYTES) {  // no bound short of the whole buffer
+    cur = walk_window(buf, len, I, pos, len, max_n, threads_for(span), W);
+    for (const auto &sl : W.plan) have += sl.cnt;
+  } else {
+    cur.pos = pos;
+    uint64_t p0 = pos;
+    bool first = true;
+    while (!cur.stopped && cur.pos < len && have < max_n) {
+      uint64_t end;
+      if (first) {  // learn the record sizes
+        end = len;
+        const size_t r = W.used++;
+        walk(buf, len, I, cur.pos, len, std::min<uint64_t>(256, max_n), stretch(W, r), cur);
+        W.plan.push_back(PcapSlice{r, 0, W.R[r].size()});
+        have += W.R[r].size();
+        if (cur.stopped && cur.stop == GPD_PCAP_STOP_LIMIT) cur.stopped = false;
+        first = false;
+        continue;
+      }
+      const double mean = have ? (double)(cur.pos - p0) / (double)have : 96.0;
+      const uint64_t want = (uint64_t)((double)(max_n - have) * mean * 1.25) + 4096;
+      end = std::min<uint64_t>(len, cur.pos + want);
+      cur = walk_window(buf, len, I, cur.pos, end, max_n - have, threads_for(end - cur.pos), W);
+      have = 0;
+      for (const auto &sl : W.plan) have += sl.cnt;
+      if (cur.stopped && cur.stop == GPD_PCAP_STOP_LIMIT) cur.stopped = false;
+    }
+  }
+  if (!cur.stopped && cur.pos >= len) {  // the walk reached the end: the next header starts exactly there
     cur.stop = GPD_PCAP_STOP_EOF;
     cur.stopped = true;
   }
@@ -212,14 +398,12 @@ int pcap_walk(const uint8_t *buf, uint64_t len, const gpd_pcap_info &I, uint64_t
       const size_t at = (size_t)(&sl - W.plan.data());
       cur.pos = W.R[sl.r].pos[sl.j0 + sl.cnt];
       W.plan.resize(at + 1);
-      cur.stop = GPD_PCAP_STOP_LIMIT;
-      cur.a0 = cur.a1 = 0;
       n = max_n;
       break;
     }
     n += sl.cnt;
   }
-  if (n == max_n && cur.stop != GPD_PCAP_STOP_LIMIT) {  // as the sequential loop: the limit first
+  if (n == max_n) {  // as the sequential loop: the limit first
     cur.stop = GPD_PCAP_STOP_LIMIT;
     cur.a0 = cur.a1 = 0;
   }
@@ -330,6 +514,15 @@ int gpd_pcap_index(const uint8_t *buf, uint64_t len, const gpd_pcap_info *info, 
   if (next_pos) *next_pos = W.next_pos;
   if (stop) *stop = W.stop;
   return rc;
+}
+
+int gpd_pcap_locate(const uint8_t *buf, uint64_t len, const gpd_pcap_info *info, uint64_t pos,
+                    const uint64_t *targets, uint64_t k, uint64_t *pos_out, uint64_t *n_total, int *stop,
+                    int nthreads) {
+  if (!info || (!buf && len) || (k && (!targets || !pos_out)))
+    return gpd::set_error(GPD_ERR_INVALID, "gpd_pcap_locate: null argument");
+  if (pos > len) return gpd::set_error(GPD_ERR_INVALID, "gpd_pcap_locate: pos beyond the buffer");
+  return gpd::pcap_locate(buf, len, *info, pos, targets, k, pos_out, n_total, stop, nthreads);
 }
 
 void gpd_pcap_last_stats(int *threads, int *met, int *rewalks) {

@@ -609,6 +609,20 @@ static int alloc_slots(gpd_ctx *ctx, uint64_t bytes, uint64_t pkts, bool ext) {
   return GPD_OK;
 }
 
+// Error exits of the staged paths leave no slot in flight: every busy slot is waited for and
+// dropped (its results belong to the failed call and are not drained anywhere), so the next
+// call on the context starts from idle slots.  On success every slot was drained already.
+struct SlotGuard {
+  gpd_ctx *ctx;
+  ~SlotGuard() {
+    for (auto &s : ctx->slot)
+      if (s.busy) {
+        (void)hipStreamSynchronize(s.stream);
+        s.busy = false;
+      }
+  }
+};
+
 static void drain_slot(gpd_ctx::Slot &s, const gpd_result *out) {
   const uint64_t m = s.hi - s.lo;
   par_for(m, 1u << 16, [&](uint64_t a, uint64_t b) {
@@ -633,6 +647,7 @@ int gpd_decode_host(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out) {
   const uint64_t kPkts = 1u << 20, kBytes = 256ull << 20;
   int rc = alloc_slots(ctx, kBytes, kPkts, out->ext != nullptr);
   if (rc) return rc;
+  SlotGuard guard{ctx};
   uint64_t i = 0;
   int k = 0;
   while (i < in->n) {
@@ -770,20 +785,30 @@ static void par_memcpy(uint8_t *dst, const uint8_t *src, uint64_t n, int nthread
 int gpd_decode_pcap(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, uint64_t max_n,
                     const gpd_result *out, uint64_t *n_out, uint64_t *next_pos, int *stop,
                     int nthreads) {
-  if (!ctx || !buf || !out || !out->status || !out->layers || !n_out)
+  if (!ctx || !buf) return set_err(GPD_ERR_INVALID, "gpd_decode_pcap: null argument");
+  gpd_pcap_info info;
+  const int rc = gpd_pcap_header(buf, len, &info);
+  if (rc) return rc;
+  return gpd_decode_pcap_at(ctx, buf, len, &info, GPD_PCAP_HEADER_BYTES, max_n, out, n_out, next_pos, stop,
+                            nthreads);
+}
+
+int gpd_decode_pcap_at(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, const gpd_pcap_info *info,
+                       uint64_t pos, uint64_t max_n, const gpd_result *out, uint64_t *n_out,
+                       uint64_t *next_pos, int *stop, int nthreads) {
+  if (!ctx || !buf || !info || !out || !out->status || !out->layers || !n_out)
     return set_err(GPD_ERR_INVALID, "gpd_decode_pcap: null argument");
   if (out->ext) return set_err(GPD_ERR_INVALID, "gpd_decode_pcap: ext records not supported");
+  if (pos > len) return set_err(GPD_ERR_INVALID, "gpd_decode_pcap_at: pos beyond the buffer");
   if (nthreads <= 0) nthreads = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
-  gpd_pcap_info info;
-  int rc = gpd_pcap_header(buf, len, &info);
-  if (rc) return rc;
+  int rc;
   // The walk and its flattened positions are kept per thread across calls (a replay or
   // capture loop calls again and again; fresh pages for 24 B per record cost more than the
   // walk itself).
   static thread_local gpd::PcapWalk W;
   static thread_local std::vector<uint64_t> rp;
   static thread_local std::vector<uint32_t> rcap;
-  const int wrc = gpd::pcap_walk(buf, len, info, GPD_PCAP_HEADER_BYTES, max_n, nthreads, W);
+  const int wrc = gpd::pcap_walk(buf, len, *info, pos, max_n, nthreads, W);
   std::string werr = wrc ? std::string(g_err) : std::string();
   const uint64_t n = W.n;
   if (rp.size() < n) {
@@ -798,7 +823,7 @@ int gpd_decode_pcap(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, uint64_t max
   const uint64_t kPkts = 1u << 20, kBytes = 256ull << 20;
   rc = alloc_slots(ctx, kBytes, kPkts, false);
   if (rc) return rc;
-  const bool pinned = ctx->is_registered(buf, len);
+  SlotGuard guard{ctx};
   uint64_t i = 0;
   int k = 0;
   while (i < n) {
@@ -824,7 +849,7 @@ int gpd_decode_pcap(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, uint64_t max
       std::memcpy(s.h_len + a, RC + a, (b - a) * 4);
     });
     const uint8_t *src = buf + base;
-    if (!pinned) {
+    if (!ctx->is_registered(src, span)) {  // (a shard registers only its own bytes)
       par_memcpy(s.h_data, src, span, nthreads);
       src = s.h_data;
     }

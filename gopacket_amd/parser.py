@@ -302,6 +302,28 @@ class DecodingLayerParser:
                           res.csum[:k], None, res.hdr_off[:k])
         return out, k, err
 
+    def DecodePcapAt(self, cap: np.ndarray, info, pos: int, max_n: int, out: BatchResult,
+                     nthreads: int = 0, data_len: Optional[int] = None):
+        """The ReadPacketData loop continued from record header `pos` (gpd_decode_pcap_at): the
+        next max_n records decoded into `out` (a BatchResult with hdr_off and at least max_n
+        entries, reused across calls).  Returns (records decoded, next record position, STOP_*,
+        error text or None)."""
+        dl = cap.shape[0] - PAD if data_len is None else int(data_len)
+        if len(out.status) < max_n or out.hdr_off is None:
+            raise ValueError("DecodePcapAt: out must hold max_n entries, with hdr_off")
+        r = GpdResult(out.status.ctypes.data, out.layers.ctypes.data, out.net_hash.ctypes.data,
+                      out.tp_hash.ctypes.data, out.csum.ctypes.data, None, out.hdr_off.ctypes.data)
+        n, nxt, stop = C.c_uint64(), C.c_uint64(), C.c_int()
+        rc = lib.gpd_decode_pcap_at(self.ctx().h, cap.ctypes.data, dl, C.byref(info), int(pos),
+                                    int(max_n), C.byref(r), C.byref(n), C.byref(nxt), C.byref(stop),
+                                    int(nthreads))
+        err = None
+        if rc == GPD_ERR_PCAP:
+            err = lib.gpd_last_error_string().decode()
+        elif rc != 0:
+            check(rc, "gpd_decode_pcap_at")
+        return n.value, nxt.value, stop.value, err
+
     def DecodeTPv3(self, ring, max_n: int = 1 << 20, max_blocks: Optional[int] = None,
                    add_vlan_header: bool = False, nthreads: int = 0, out=None, ci=None):
         """Every packet of the user-owned blocks of a TPACKET_V3 ring (afpacket.TPv3Ring) from

@@ -69,11 +69,12 @@ def header(cap: np.ndarray, n: Optional[int] = None) -> GpdPcapInfo:
 
 
 def index(cap: np.ndarray, max_n: Optional[int] = None, nthreads: int = 0,
-          data_len: Optional[int] = None) -> Pcap:
-    """Index every record of a capture array (capture_array()) — the ReadPacketData loop."""
+          data_len: Optional[int] = None, pos: int = 24) -> Pcap:
+    """Index every record of a capture array (capture_array()) — the ReadPacketData loop —
+    from record header position `pos` (24: the first record)."""
     dl = cap.shape[0] - PAD if data_len is None else int(data_len)
     info = header(cap, dl)
-    cap_n = (dl - 24) // 16 + 1 if max_n is None else int(max_n)
+    cap_n = (dl - pos) // 16 + 1 if max_n is None else int(max_n)
     off = np.empty(cap_n, np.uint32)
     ln = np.empty(cap_n, np.uint32)
     wl = np.empty(cap_n, np.uint32)
@@ -81,7 +82,7 @@ def index(cap: np.ndarray, max_n: Optional[int] = None, nthreads: int = 0,
     n = C.c_uint64()
     nxt = C.c_uint64()
     stop = C.c_int()
-    rc = lib.gpd_pcap_index(cap.ctypes.data, dl, C.byref(info), 24, cap_n, off.ctypes.data,
+    rc = lib.gpd_pcap_index(cap.ctypes.data, dl, C.byref(info), int(pos), cap_n, off.ctypes.data,
                             ln.ctypes.data, wl.ctypes.data, ts.ctypes.data, C.byref(n),
                             C.byref(nxt), C.byref(stop), int(nthreads))
     err = None
@@ -93,6 +94,27 @@ def index(cap: np.ndarray, max_n: Optional[int] = None, nthreads: int = 0,
     batch = PacketBatch(cap, dl, off[:k], ln[:k])
     return Pcap(batch, ts[:k], wl[:k], info.linktype, info.snaplen, bool(info.nano),
                 stop.value, nxt.value, err)
+
+
+def locate(cap: np.ndarray, targets, pos: int = 24, data_len: Optional[int] = None,
+           nthreads: int = 0, info: Optional[GpdPcapInfo] = None):
+    """gpd_pcap_locate: header positions of records `targets` (ascending record numbers of the
+    ReadPacketData walk from `pos`) with one parallel counting pass and no per-record arrays.
+    Returns (positions uint64[len(targets)], records in the walk, STOP_* of its end)."""
+    dl = cap.shape[0] - PAD if data_len is None else int(data_len)
+    info = header(cap, dl) if info is None else info
+    t = np.ascontiguousarray(np.asarray(targets, dtype=np.uint64))
+    out = np.zeros(len(t), np.uint64)
+    n, stop = C.c_uint64(), C.c_int()
+    check(lib.gpd_pcap_locate(cap.ctypes.data, dl, C.byref(info), int(pos), t.ctypes.data, len(t),
+                              out.ctypes.data, C.byref(n), C.byref(stop), int(nthreads)),
+          "gpd_pcap_locate")
+    return out, n.value, stop.value
+
+
+def shard_bounds(n_records: int, world: int):
+    """Record ranges [g*N/G, (g+1)*N/G) of the G shards of an N-record capture."""
+    return [(n_records * g // world, n_records * (g + 1) // world) for g in range(world)]
 
 
 def last_walk_stats():

@@ -135,6 +135,40 @@ def make_udp64(n: int, seed: int = 0x5EED0002, chunk: int = 1 << 20) -> PacketBa
                        np.full(n, 64, dtype=np.uint32))
 
 
+_native = None
+
+
+def _native_lib():
+    """gopacket_amd/libgpd_synth.so (csrc/synth/gpd_synth.c): make_udp64's bytes, natively."""
+    global _native
+    if _native is None:
+        import ctypes as C
+        import os
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgpd_synth.so")
+        if not os.path.exists(path):
+            from .build import build_synth
+            build_synth()
+        L = C.CDLL(path)
+        L.gpds_udp64.restype = None
+        L.gpds_udp64.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_void_p,
+                                 C.c_uint32, C.c_int, C.c_int]
+        _native = L
+    return _native
+
+
+def udp64_native(dst: np.ndarray, lo: int, hi: int, seed: int = 0x5EED0002, records: bool = False,
+                 nthreads: int = 16) -> None:
+    """Packets [lo, hi) of make_udp64(seed) into dst (a uint8 array or a view of one): 64 B back
+    to back, or as pcap records (16-B header {i // 10^6, i % 10^6, 64, 64} + 64 B, the framing
+    of pcap.synth_capture) when `records`."""
+    need = (hi - lo) * (80 if records else 64)
+    if dst.dtype != np.uint8 or dst.size < need or not dst.flags.c_contiguous:
+        raise ValueError("udp64_native: dst must be a contiguous uint8 array of the records' size")
+    free = _free_ports(TABLES.udp_port).astype(np.uint16)
+    _native_lib().gpds_udp64(dst.ctypes.data, lo, hi, seed & 0xFFFFFFFFFFFFFFFF, free.ctypes.data,
+                             len(free), int(bool(records)), int(nthreads))
+
+
 IMIX_SIZES = (64, 576, 1500)
 IMIX_WEIGHTS = (7, 4, 1)
 

@@ -101,6 +101,29 @@ int gpd_decode_pcap(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, uint64_t max
                     const gpd_result *out, uint64_t *n_out, uint64_t *next_pos, int *stop,
                     int nthreads);
 
+/* gpd_decode_pcap continued from record header position `pos` of a capture whose file header
+ * `info` was already parsed (gpd_pcap_header): the next max_n ReadPacketData records of the
+ * loop are decoded exactly as gpd_decode_pcap decodes them, and *next_pos tells where the
+ * following call continues.  This is the loop over a capture too large for one call (a
+ * replay streamed in chunks of records), and the loop over one shard of a capture: a shard's
+ * first record position comes from gpd_pcap_locate.  buf may exceed 4 GiB. */
+int gpd_decode_pcap_at(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, const gpd_pcap_info *info,
+                       uint64_t pos, uint64_t max_n, const gpd_result *out, uint64_t *n_out,
+                       uint64_t *next_pos, int *stop, int nthreads);
+
+/* Record positions without indexing: the ReadPacketData loop from `pos` with every record
+ * read and dropped.  targets[0..k) are record numbers of that walk (0 = the record at pos),
+ * ascending; pos_out[t] is the header position of record targets[t] (a target equal to the
+ * walk's record count gives the position where the walk ends).  *n_total (may be NULL) is
+ * the number of records the walk reads before its end (EOF or the first rejected record,
+ * whose kind goes to *stop, may be NULL).  A target beyond *n_total is GPD_ERR_INVALID.
+ * This is how a capture is cut by packet index into shards [g*N/G, (g+1)*N/G) (one shard
+ * per GPU) with one parallel counting pass (nthreads as gpd_pcap_index) and no
+ * per-record arrays. */
+int gpd_pcap_locate(const uint8_t *buf, uint64_t len, const gpd_pcap_info *info, uint64_t pos,
+                    const uint64_t *targets, uint64_t k, uint64_t *pos_out, uint64_t *n_total, int *stop,
+                    int nthreads);
+
 /* Diagnostics of this thread's last walk: segments walked in parallel, segments whose
  * speculation the true walk met, segments re-walked sequentially. */
 void gpd_pcap_last_stats(int *threads, int *met, int *rewalks);

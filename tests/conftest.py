@@ -15,8 +15,9 @@ def pytest_configure(config):
 @pytest.fixture(scope="session", autouse=True)
 def _built_libs():
     """Build libgpd.so (hipcc, gfx950) and the oracle if their sources are newer."""
-    from gopacket_amd.build import build_abi_host, build_lib, build_oracle
+    from gopacket_amd.build import build_abi_host, build_lib, build_oracle, build_synth
     build_oracle()
+    build_synth()
     if os.path.exists("/opt/rocm/bin/hipcc"):
         build_lib()
         build_abi_host()

@@ -177,3 +177,110 @@ def test_limit_and_resume():
     assert p.batch.n == 1234 and p.stop == NP.STOP_LIMIT and p.err is None
     recs, _, _, _ = R.walk(buf)
     assert p.next_pos == recs[1234][0] - 16
+
+
+# ---- bounded walks, record location and shards (config 5: one capture cut by packet index) ----
+def _oracle_positions(buf):
+    recs, stop, nxt, err = R.walk(buf)
+    return np.array([r[0] - 16 for r in recs], dtype=np.uint64), stop, nxt
+
+
+@pytest.mark.parametrize("maker", ["imix", "decoys"])
+def test_bounded_walk_windows(maker):
+    """A bounded walk (max_n records from any record position) goes window by window in parallel;
+    every window size must give the sequential loop's records, next position and stop."""
+    if maker == "imix":
+        buf, _ = _big_capture(1 << 15, seed=5)
+    else:
+        rng = np.random.default_rng(9)
+        decoy = b"".join(struct.pack("<IIII", 1, 2, L, L) + bytes(L) for L in rng.integers(4, 40, 64))
+        pkts = [decoy[k % 97:][:900 + (k % 400)] for k in range(9000)]
+        buf = NP.synth_capture(PacketBatch.from_packets(pkts, align=1))[:-NP.PAD].tobytes()
+    pos, _, _ = _oracle_positions(buf)
+    cap = NP.capture_array(buf)
+    N = len(pos)
+    for start in (0, 1, 777, N // 2):
+        for m in (1, 300, 5000, N // 3, N - start, N - start + 10):
+            p = NP.index(cap, max_n=m, nthreads=8, pos=int(pos[start]))
+            k = min(m, N - start)
+            assert p.batch.n == k
+            assert np.array_equal(p.batch.offset.astype(np.uint64), pos[start:start + k] + 16)
+            if start + k < N:
+                assert p.stop == NP.STOP_LIMIT and p.next_pos == pos[start + k]
+            elif m == k:
+                assert p.stop == NP.STOP_LIMIT and p.next_pos == len(buf)
+            else:
+                assert p.stop == NP.STOP_EOF and p.next_pos == len(buf)
+
+
+def test_bounded_walk_stops_at_rejected_record():
+    buf, _ = _big_capture(1 << 15, seed=13)
+    buf = bytearray(buf)
+    pos, _, _ = _oracle_positions(bytes(buf))
+    k = len(pos) * 3 // 4
+    struct.pack_into("<II", buf, int(pos[k]) + 8, 262145, 262145)
+    cap = NP.capture_array(bytes(buf))
+    p = NP.index(cap, max_n=k - 100 + 5000, nthreads=8, pos=int(pos[100]))
+    assert p.batch.n == k - 100 and p.next_pos == pos[k]
+    assert p.err == "capture length exceeds snap length: 262145 > 262144"
+
+
+@pytest.mark.parametrize("threads", [1, 3, 8])
+def test_locate_matches_sequential_walk(threads):
+    buf, _ = _big_capture(1 << 15, seed=17)
+    pos, _, _ = _oracle_positions(buf)
+    cap = NP.capture_array(buf)
+    N = len(pos)
+    targets = [0, 1, 2, 4095, 4096, 10000, N // 2, N - 1, N]
+    got, n, stop = NP.locate(cap, targets, nthreads=threads)
+    assert n == N and stop == NP.STOP_EOF
+    want = [int(pos[t]) if t < N else len(buf) for t in targets]
+    assert list(got) == want
+    # from a record position inside the capture
+    got2, n2, _ = NP.locate(cap, [0, 5, N - 1000], pos=int(pos[1000]), nthreads=threads)
+    assert n2 == N - 1000 and list(got2) == [int(pos[1000]), int(pos[1005]), len(buf)]
+    with pytest.raises(Exception, match="beyond"):
+        NP.locate(cap, [N + 1], nthreads=threads)
+
+
+def test_locate_stops_at_rejected_record():
+    buf, _ = _big_capture(1 << 15, seed=19)
+    buf = bytearray(buf)
+    pos, _, _ = _oracle_positions(bytes(buf))
+    k = len(pos) // 3
+    struct.pack_into("<I", buf, int(pos[k]) + 12, 1)  # wire length < caplen
+    got, n, stop = NP.locate(NP.capture_array(bytes(buf)), [0, k // 2, k], nthreads=8)
+    assert n == k and stop == NP.STOP_ORIGLEN
+    assert list(got) == [int(pos[0]), int(pos[k // 2]), int(pos[k])]
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_shards_partition_the_capture(world):
+    """Config 5's cut: shard g = records [g*N/G, (g+1)*N/G), located in one counting pass and
+    indexed from its first record; the shards are disjoint and together are the whole index."""
+    buf, b = _big_capture(1 << 15, seed=23)
+    cap = NP.capture_array(buf)
+    whole = NP.index(cap, nthreads=8)
+    N = whole.batch.n
+    bounds = NP.shard_bounds(N, world)
+    starts, n, _ = NP.locate(cap, [lo for lo, _ in bounds] + [N], nthreads=8)
+    assert n == N
+    parts = []
+    for g, (lo, hi) in enumerate(bounds):
+        p = NP.index(cap, max_n=hi - lo, nthreads=8, pos=int(starts[g]))
+        assert p.batch.n == hi - lo and p.next_pos == starts[g + 1]
+        parts.append(p.batch.offset)
+    cat = np.concatenate(parts)
+    assert len(np.unique(cat)) == N
+    assert np.array_equal(cat, whole.batch.offset)
+
+
+def test_bounded_walk_runs_windows_in_parallel():
+    buf, _ = _big_capture(1 << 15, seed=29)
+    pos, _, _ = _oracle_positions(buf)
+    cap = NP.capture_array(buf)
+    N = len(pos)
+    p = NP.index(cap, max_n=N - 1, nthreads=8)
+    assert p.batch.n == N - 1 and p.next_pos == pos[N - 1]
+    assert np.array_equal(p.batch.offset.astype(np.uint64), pos[:N - 1] + 16)
+    assert NP.last_walk_stats()[0] > 1
