@@ -69,11 +69,13 @@ def header(cap: np.ndarray, n: Optional[int] = None) -> GpdPcapInfo:
 
 
 def index(cap: np.ndarray, max_n: Optional[int] = None, nthreads: int = 0,
-          data_len: Optional[int] = None, pos: int = 24) -> Pcap:
+          data_len: Optional[int] = None, pos: int = 24, info: Optional[GpdPcapInfo] = None) -> Pcap:
     """Index every record of a capture array (capture_array()) — the ReadPacketData loop —
-    from record header position `pos` (24: the first record)."""
+    from record header position `pos` (24: the first record).  `info`: the capture's parsed
+    file header, for a window of a capture (cap = a view from some record on; offsets are
+    relative to the view)."""
     dl = cap.shape[0] - PAD if data_len is None else int(data_len)
-    info = header(cap, dl)
+    info = header(cap, dl) if info is None else info
     cap_n = (dl - pos) // 16 + 1 if max_n is None else int(max_n)
     off = np.empty(cap_n, np.uint32)
     ln = np.empty(cap_n, np.uint32)

@@ -60,15 +60,18 @@ def lib():
 
 
 def decode(batch, first: int = 17, decoders: int = 0x3FF, options: int = 0,
-           tables: DispatchTables | None = None, ext: bool = True, nthreads: int = 1) -> BatchResult:
-    """Oracle decode of a PacketBatch; same output words as the device path."""
+           tables: DispatchTables | None = None, ext: bool = True, nthreads: int = 1,
+           out: BatchResult | None = None) -> BatchResult:
+    """Oracle decode of a PacketBatch; same output words as the device path.  `out` (a
+    BatchResult of batch.n entries with hdr_off, ext as requested) is reused when given."""
     t = tables or TABLES
     tabs = _Tables(t.ethertype.ctypes.data, t.ipproto.ctypes.data, t.tcp_port.ctypes.data,
                    t.udp_port.ctypes.data)
     n = batch.n
-    res = BatchResult(np.zeros(n, np.uint32), np.zeros(n, np.uint64), np.zeros(n, np.uint64),
-                      np.zeros(n, np.uint64), np.zeros(n, np.uint32),
-                      np.zeros(n, EXT_DTYPE) if ext else None, np.zeros(n, np.uint32))
+    res = out if out is not None else BatchResult(
+        np.zeros(n, np.uint32), np.zeros(n, np.uint64), np.zeros(n, np.uint64),
+        np.zeros(n, np.uint64), np.zeros(n, np.uint32),
+        np.zeros(n, EXT_DTYPE) if ext else None, np.zeros(n, np.uint32))
     lib().gpo_decode_batch(batch.data.ctypes.data, batch.offset.ctypes.data, batch.caplen.ctypes.data,
                            n, first, decoders, options, C.byref(tabs), res.status.ctypes.data,
                            res.layers.ctypes.data, res.net_hash.ctypes.data, res.tp_hash.ctypes.data,
