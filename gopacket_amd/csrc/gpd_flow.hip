@@ -59,6 +59,7 @@ struct FlowParams {
   // insert -> verify: bit l of word w set when packet 64w+l claimed its record (and so wrote
   // the key the verify would compare against); one word per wave iteration
   uint64_t *made = nullptr;
+  uint64_t fp_mask = ~0ull;  // gpd_flow_test_fingerprint_bits (all ones in production)
 };
 
 // The key of packet i as 10 words: src[16], dst[16], ports (raw wire bytes), types.  Returns
@@ -92,7 +93,7 @@ __device__ __forceinline__ bool flow_key(const FlowParams &P, uint64_t i, uint32
   return true;
 }
 
-__device__ __forceinline__ uint64_t fingerprint(const uint32_t (&k)[10]) {
+__device__ __forceinline__ uint64_t fingerprint(const uint32_t (&k)[10], uint64_t mask) {
   uint64_t h = 0x9E3779B97F4A7C15ull;
 #pragma unroll
   for (int w = 0; w < 10; w += 2) {
@@ -103,6 +104,7 @@ __device__ __forceinline__ uint64_t fingerprint(const uint32_t (&k)[10]) {
   h ^= h >> 33;
   h *= 0xC4CEB9FE1A85EC53ull;
   h ^= h >> 33;
+  h &= mask;
   return h ? h : 1ull;
 }
 
@@ -217,7 +219,7 @@ __global__ __launch_bounds__(kFlowThreads) void flow_insert_kernel(FlowParams P)
     // probe sequence to the same record: only the first lane of each such run probes, and
     // the others take its slot afterwards.
     const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t fp = keyed ? fingerprint(k) : 0ull;  // fingerprints are never 0
+    const uint64_t fp = keyed ? fingerprint(k, P.fp_mask) : 0ull;  // fingerprints are never 0
     const uint64_t fp_prev = __shfl_up(fp, 1u, 64);
     const uint64_t lead = __ballot(!keyed || lane == 0u || fp_prev != fp);
     const bool probes = keyed && ((lead >> lane) & 1ull);
@@ -417,7 +419,7 @@ __global__ __launch_bounds__(kFlowThreads) void flow_part_scatter_kernel(FlowPar
       r.caplen = P.caplen[i];
       r.owner = o;
       r.seq = P.base + i;
-      r.fp = fingerprint(k);
+      r.fp = fingerprint(k, P.fp_mask);
       P.kout[start[o] + slot] = r;
     }
   }
@@ -484,6 +486,7 @@ struct gpd_flowtable {
   uint64_t parts_words = 0;
   uint64_t *made = nullptr;  // insert -> verify claim bits, one word per 64 packets, grown on use
   uint64_t made_words = 0;
+  uint64_t fp_mask = ~0ull;  // gpd_flow_test_fingerprint_bits
 };
 
 #define FLOW_TRY(expr)                                                                      \
@@ -570,6 +573,7 @@ int gpd_flow_insert(gpd_flowtable *ft, const gpd_batch *in, const gpd_result *re
                     nullptr, nullptr, nullptr, nullptr, nullptr, 0};
   FLOW_TRY(grow_made(ft, in->n));
   P.made = ft->made;
+  P.fp_mask = ft->fp_mask;
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid(grid_for(in->n, ft->num_cus)), block(gpd::kFlowThreads);
   hipLaunchKernelGGL(gpd::flow_insert_kernel<false>, grid, block, 0, s, P);
@@ -607,6 +611,7 @@ int gpd_flow_keys(gpd_flowtable *ft, const gpd_batch *in, const gpd_result *res,
   gpd::FlowParams P{in->data, in->data_len, in->offset, in->caplen, res->status, res->hdr_off,
                     nullptr, in->n, index_base, ft->tab, ft->cap - 1, ft->stats,
                     nullptr, res->net_hash, res->tp_hash, keys, ft->parts, nparts};
+  P.fp_mask = ft->fp_mask;
   hipLaunchKernelGGL(gpd::flow_part_count_kernel, grid, block, 0, s, P);
   FLOW_TRY(hipGetLastError());
   hipLaunchKernelGGL(gpd::flow_part_scan_kernel, dim3(1), dim3(1024), 0, s, ft->parts, L, nparts, grid.x);
@@ -649,6 +654,7 @@ int gpd_flow_insert_keys(gpd_flowtable *ft, const gpd_flow_key *keys, uint64_t n
                     ft->cap - 1, ft->stats, keys, nullptr, nullptr, nullptr, nullptr, 0};
   FLOW_TRY(grow_made(ft, n));
   P.made = ft->made;
+  P.fp_mask = ft->fp_mask;  // (key records carry their sender's fingerprint; recomputed here)
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid(grid_for(n, ft->num_cus)), block(gpd::kFlowThreads);
   hipLaunchKernelGGL(gpd::flow_insert_kernel<true>, grid, block, 0, s, P);
@@ -712,6 +718,13 @@ int gpd_flow_export(gpd_flowtable *ft, gpd_flow_rec *out, uint32_t *rec_index, u
     if (rec_index) rec_index[j] = idx[order[j]];
   }
   *n = m;
+  return GPD_OK;
+}
+
+int gpd_flow_test_fingerprint_bits(gpd_flowtable *ft, uint32_t bits) {
+  if (!ft || bits == 0 || bits > 64)
+    return gpd::set_error(GPD_ERR_INVALID, "gpd_flow_test_fingerprint_bits: bits %u outside [1, 64]", bits);
+  ft->fp_mask = bits == 64 ? ~0ull : (1ull << bits) - 1ull;
   return GPD_OK;
 }
 

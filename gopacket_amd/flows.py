@@ -71,6 +71,11 @@ class FlowTable:
                                   int(index_base), self._stream(stream)), "gpd_flow_insert")
         return flow_id
 
+    def _test_fingerprint_bits(self, bits: int) -> None:
+        """Testing hook (gpd_flow_test_fingerprint_bits): narrow every key fingerprint to
+        `bits` bits so that distinct keys collide; call on an empty table."""
+        check(lib.gpd_flow_test_fingerprint_bits(self.h, int(bits)), "gpd_flow_test_fingerprint_bits")
+
     def Stats(self, stream=None) -> dict:
         st = FlowStats()
         check(lib.gpd_flow_stats_get(self.h, C.byref(st), self._stream(stream)), "gpd_flow_stats_get")

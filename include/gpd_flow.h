@@ -91,6 +91,11 @@ int gpd_flow_stats_get(gpd_flowtable *ft, gpd_flow_stats *out, void *stream);
 int gpd_flow_export(gpd_flowtable *ft, gpd_flow_rec *out, uint32_t *rec_index, uint64_t max,
                     uint64_t *n, void *stream);
 int gpd_flow_destroy(gpd_flowtable *ft);
+/* Testing hook: keep only the low `bits` (1..64) bits of every key fingerprint (64 = the
+ * default) from the next insert on, so that distinct keys share fingerprints and the
+ * collision path (GPD_FLOW_COLLISION, gpd_flow_stats.collisions) runs.  Call it on an empty
+ * table (after create or reset); a production table never calls it. */
+int gpd_flow_test_fingerprint_bits(gpd_flowtable *ft, uint32_t bits);
 
 /* ---- flow-affine sharding over several GPUs ----
  * The reference's fan-out idiom sends every packet of a flow to one worker picked by the

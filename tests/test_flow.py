@@ -284,3 +284,46 @@ def test_sharded_flow_table_two_ranks():
         assert (int(rec["first"]), int(rec["last"]), int(rec["packets"]), int(rec["bytes"])) == \
             (f["first"], f["last"], f["packets"], f["bytes"])
     assert all(len(t) > 0 for t in tables)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits", [3, 12])
+def test_flow_fingerprint_collisions_are_flagged(bits):
+    """Fingerprints narrowed to a few bits (test hook): distinct keys now share records.  A
+    packet whose key differs from its record's stored key (the claimer's) must carry
+    GPD_FLOW_COLLISION, every other packet must not, the collision counter must count exactly
+    the flagged packets, and each record's counters still cover every packet mapped to it."""
+    import torch
+    from gopacket_amd import flows as FL
+    from gopacket_amd import parser as P
+    batch = synth.make_mixed(20000)
+    parser = P.NewDecodingLayerParser(L.LayerTypeEthernet, *[P.DECODER_BY_NAME[k]() for k in P.DECODER_BY_NAME])
+    db, dr = _decode_dev(parser, batch)
+    ft = FL.NewFlowTable(parser, 1 << 16)
+    ft._test_fingerprint_bits(bits)
+    fid = ft.Insert(db, dr).cpu().numpy().view(np.uint32)
+    torch.cuda.synchronize()
+    ref = O.decode(batch, L.LayerTypeEthernet, parser.decoders, 0, ext=False, nthreads=8)
+    flows_ref, per_ref = F.group(batch, ref)
+    keyed = np.array([k is not None for k in per_ref])
+    assert ((fid == 0xFFFFFFFF) == ~keyed).all()
+    rec_of = fid & 0x7FFFFFFF
+    flagged = (fid & 0x80000000) != 0
+    recs, idx = ft.Export()
+    st = ft.Stats()
+    assert st["flows"] == len(recs) <= (1 << bits) and st["full"] == 0
+    assert len(recs) < len(flows_ref)  # keys were merged
+    stored = {int(ix): F.record_key(r) for r, ix in zip(recs, idx)}
+    ki = np.nonzero(keyed)[0]
+    for i in ki:
+        assert flagged[i] == (per_ref[i] != stored[int(rec_of[i])])
+    assert st["collisions"] == int(flagged.sum()) > 0
+    # a key always lands on one record; each record counts every packet that landed on it
+    rec_by_key = {}
+    for i in ki:
+        assert rec_by_key.setdefault(per_ref[i], int(rec_of[i])) == int(rec_of[i])
+    for r, ix in zip(recs, idx):
+        on = ki[rec_of[ki] == ix]
+        assert int(r["packets"]) == len(on)
+        assert int(r["bytes"]) == int(batch.caplen[on].astype(np.int64).sum())
+        assert (int(r["first"]), int(r["last"])) == (int(on.min()), int(on.max()))

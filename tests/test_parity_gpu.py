@@ -286,3 +286,56 @@ def test_full_size_config2_properties():
         assert np.array_equal(getattr(res, f)[idx], getattr(ref, f)), f
     del res
     torch.cuda.empty_cache()
+
+
+def _full_size_common(b, res, want_decoded, ip_off, n):
+    """Properties every packet of a full-size synthetic config shares, plus a strided sample
+    bit-exact against the oracle."""
+    assert np.all(res.status & 3 == 0), "every packet decodes cleanly"
+    assert np.all(((res.status >> 4) & 31) == len(want_decoded))
+    assert np.all(res.layers == res.layers[0]), "one decoded stack for all"
+    assert res.decoded(0) == want_decoded
+    bad = (np.arange(n) % 64) == 63  # synth: 1 in 64 carries a corrupted TCP checksum
+    assert np.array_equal((res.csum >> 16) != 0, bad), "TCP ComputeChecksum is 0 exactly when valid"
+    off = b.offset.astype(np.int64) + ip_off + 10
+    stored = (b.data[off].astype(np.uint32) << 8) | b.data[off + 1]
+    assert np.array_equal(res.csum & 0xFFFF, stored), "IPv4 header checksum equals the stored one"
+    idx = np.arange(0, n, 2039)
+    sb = PacketBatch(b.data, b.data_len, b.offset[idx].copy(), b.caplen[idx].copy())
+    ref = O.decode(sb, ext=False, nthreads=8)
+    for f in ("status", "layers", "net_hash", "tp_hash", "csum"):
+        assert np.array_equal(getattr(res, f)[idx], getattr(ref, f)), f
+
+
+def test_full_size_config3_imix_properties():
+    """BASELINE config 3 at full size (2^22 IMIX 64/576/1500 Eth/Dot1Q/IPv4/TCP): every window
+    class, multi-window tiles and the wave-cooperative transport checksum at their real mix."""
+    import torch
+    from gopacket_amd import parser as P
+    n = 1 << 22
+    b = synth.make_imix(n)
+    p = P.DecodingLayerParser(L.LayerTypeEthernet)
+    p._mask = ALL
+    res = p.DecodeBatch(b, ext=False)
+    _full_size_common(b, res, [17, 15, 20, 44, 2], 18, n)
+    assert len(np.unique(res.net_hash)) > n // 2 and len(np.unique(res.tp_hash)) > n // 4
+    del res
+    torch.cuda.empty_cache()
+
+
+def test_full_size_config4_vxlan_properties():
+    """BASELINE config 4 at full size (2^23 x 128 B VXLAN): the two-pass stack
+    [Eth, IPv4, UDP, VXLAN, Eth, IPv4, TCP, Payload] on every packet, inner flow keys (A11)."""
+    import torch
+    from gopacket_amd import parser as P
+    n = 1 << 23
+    b = synth.make_vxlan(n)
+    p = P.DecodingLayerParser(L.LayerTypeEthernet)
+    p._mask = ALL
+    res = p.DecodeBatch(b, ext=False)
+    _full_size_common(b, res, [17, 20, 45, 116, 17, 20, 44, 2], 64, n)
+    # the flow keys are the inner 5-tuple: the inner addresses and ports of packet 0
+    ref0 = O.decode(PacketBatch.from_packets([b.packet(0)[50:]]), ext=False)
+    assert int(res.net_hash[0]) == int(ref0.net_hash[0]) and int(res.tp_hash[0]) == int(ref0.tp_hash[0])
+    del res
+    torch.cuda.empty_cache()
