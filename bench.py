@@ -738,6 +738,8 @@ def main():
                     "(gpd_decode_tpv3, PCIe-inclusive); printed as a separate line")
     ap.add_argument("--ablate", default="", help="diagnostics only: 'nocsum', 'nohash' or both "
                     "(comma separated); never used for the reported metric")
+    ap.add_argument("--tune", default="", help="A/B only: engine tuning, e.g. 'shift=0' or "
+                    "'window_bytes=8192,reg_prefix=1' (gpd_ctx_set_tuning; never changes results)")
     ap.add_argument("--shard-check", default="", help="tests only (CPU, gloo): build the replay "
                     "capture, cut and index this rank's shard, write its record positions to DIR")
     ap.add_argument("--chunk", type=int, default=0, help="tests only: records per index chunk")
@@ -801,6 +803,8 @@ def main():
                                       P.IPv6(), P.IPv6ExtensionSkipper(), P.TCP(), P.UDP(),
                                       P.VXLAN(), P.Payload(), P.Fragment(), device=local)
     stream = torch.cuda.current_stream(local)
+    if args.tune:
+        parser.Tuning = {k: int(v) for k, v in (kv.split("=") for kv in args.tune.split(","))}
     if "nocsum" in args.ablate:
         parser.ComputeChecksums = False
     if "nohash" in args.ablate:
@@ -887,6 +891,8 @@ def main():
         out["roofline"]["traffic_write"] = int(tr["write"])
         out["roofline"]["traffic_source"] = tr["source"]
         out["roofline"]["profiled_kernel_us"] = tr["kernel_us"]
+    if args.tune:
+        out["tuning"] = parser.Tuning
     if args.ablate:
         out["ablation"] = args.ablate
         out["metric"] = "DIAGNOSTIC ablation (not the metric): " + out["metric"]

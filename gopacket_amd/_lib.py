@@ -9,9 +9,9 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("GPD_LIB_PATH") or os.path.join(_HERE, "libgpd.so")  # override: A/B only
+LIB_PATH = os.path.join(_HERE, "libgpd.so")
 
-GPD_ABI_VERSION = 3
+GPD_ABI_VERSION = 4
 GPD_OK = 0
 
 
@@ -32,6 +32,11 @@ class GpdResult(C.Structure):
                 ("hdr_off", C.c_void_p)]
 
 
+class GpdTuning(C.Structure):
+    _fields_ = [("window_bytes", C.c_uint32), ("shift", C.c_int32), ("reg_prefix", C.c_int32),
+                ("reserved", C.c_int32)]
+
+
 class GpdPcapInfo(C.Structure):
     _fields_ = [("magic", C.c_uint32), ("big_endian", C.c_uint32), ("nano", C.c_uint32),
                 ("version_major", C.c_uint32), ("version_minor", C.c_uint32),
@@ -50,6 +55,7 @@ EXPORTS = {
     "gpd_sync": (C.c_int, [C.c_void_p, C.c_void_p]),
     "gpd_ctx_set_timing": (C.c_int, [C.c_void_p, C.c_int]),
     "gpd_last_kernel_ms": (C.c_float, [C.c_void_p]),
+    "gpd_ctx_set_tuning": (C.c_int, [C.c_void_p, C.c_void_p]),
     "gpd_last_error_string": (C.c_char_p, []),
     # include/gpd_pcap.h
     "gpd_pcap_header": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(GpdPcapInfo)]),

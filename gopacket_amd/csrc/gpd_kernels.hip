@@ -40,6 +40,7 @@
 
 namespace gpd {
 
+constexpr uint64_t kGridRounds = 4;  // a launch covers at most 4 rounds of resident workgroups
 constexpr uint32_t kDiagSkipDecode = 1u << 31;  // internal diagnostic option (bench --ablate nodecode)
 constexpr uint32_t kDiagNoWait = 1u << 30;      // internal diagnostic: skip the per-tile DMA wait
 constexpr uint32_t kDiagNtLoad = 1u << 29;      // A/B: window LDS-DMA with the nt cache policy
@@ -614,8 +615,9 @@ done:
 
 // ---------------------------------------------------------------- fast path
 // Straight-line decode of the stacks that carry nearly all traffic:
-//   Ethernet [Dot1Q]{0,2} (IPv4 with IHL 5 | IPv6 without hop-by-hop) (TCP | UDP)
+//   Ethernet [Dot1Q]{0,2} (IPv4 with IHL 5 | IPv6 without hop-by-hop) (TCP | UDP | ICMPv4)
 //     [Payload | VXLAN + the same stack once more]
+//   Ethernet (802.3 length) LLC (SNAP / STP unsupported, or nothing)
 // for a packet in an LDS window, with Ethernet as the first layer.  Header offsets are
 // runtime values and every header is read straight from LDS at its own byte address
 // (gfx950 DS instructions take unaligned addresses), so one code path serves every tag
@@ -818,7 +820,7 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
     uint32_t W[16];
     load64(W, p + b + 14);
     const uint32_t et0 = be_lo(e.y), et1 = be_lo(e.z), et2 = be_lo(e.w);
-    if (et0 < 0x0600u) return false;  // 802.3 length framing
+    const bool llc = et0 < 0x0600u;  // 802.3 length framing: EthernetTypeLLC (0)
     const uint32_t t1 = tag_type(et0), t2 = t1 & tag_type(et1);
     const uint32_t l3 = b + 14 + 4 * (t1 + t2);
     if (t1) load64(W, p + l3);  // tagged: the network header is further in
@@ -837,7 +839,7 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
     const uint32_t ulen = be_lo(ty);
     const uint32_t seg = (g == 2u && ulen >= 8u && ulen <= plen) ? ulen : plen;
     // ---- round trip 2: all lookups
-    const uint32_t r0 = fix_bucket<kFixEthBase>(F.mult, et0);
+    const uint32_t r0 = fix_bucket<kFixEthBase>(F.mult, llc ? 0u : et0);
     uint32_t r1 = 0, r2 = 0;
     if (t1) {
       r1 = fix_bucket<kFixEthBase>(F.mult, et1);
@@ -849,6 +851,27 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
     const uint32_t rs = fix_bucket_at(pbase, F.mult, be_lo(tx));
     // ---- Ethernet / Dot1Q (dot1q.go:29-50), confirming the tag guesses
     put(GPD_C_ETHERNET);
+    if (llc) {  // ethernet.go:50-57: the EtherType field is the payload length
+      uint32_t pl = lim - b - 14u;
+      if (pl < et0) trunc = 1;
+      else pl = et0;
+      const uint32_t d0 = r0 & 15u;
+      if (pl == 0) break;  // empty payload: the loop stops (layers_decoder.go:71-73)
+      if (d0 == D_NONE) { stop = (r0 >> 8) & 0xFFu; break; }
+      if (d0 != D_LLC || pl < 3u) return false;  // remapped, or "LLC header too small"
+      // LLC, llc.go:31-52: DSAP / SSAP without their low bits, a one- or two-byte control
+      const uint32_t dsap = (e.y >> 16) & 0xFEu, ssap = (e.y >> 24) & 0xFEu, ctl = e.z & 0xFFu;
+      const uint32_t cl = (!(ctl & 1u) || (ctl & 3u) == 1u) ? 4u : 3u;
+      if (pl < cl) return false;
+      put(GPD_C_LLC);
+      if (pl == cl) break;
+      // NextLayerType, llc.go:61-69: SNAP, STP or Zero (a lookup of Zero misses: nil error)
+      const uint32_t nt = (dsap == 0xAAu && ssap == 0xAAu) ? (uint32_t)GPD_LT_SNAP
+                        : (dsap == 0x42u && ssap == 0x42u) ? (uint32_t)GPD_LT_STP : 0u;
+      if (nt && (g_lds[nt] & 15u) != D_NONE) return false;
+      stop = nt;
+      break;
+    }
     if (((r0 & 15u) == D_DOT1Q) != (t1 != 0)) return false;
     uint32_t r = r0;
     if (t1) {
@@ -906,6 +929,14 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
     // ---- transport, confirming the protocol guess
     const uint32_t d4 = (pv >> 16) & 15u;
     if (d4 == D_NONE) { stop = pv & 0xFFFFu; break; }
+    if (d4 == D_ICMP4) {  // icmp4.go:220-231; NextLayerType is Payload (:261-263)
+      if (plen < 8u) return false;  // "ICMP layer less then 8 bytes": generic path
+      put(GPD_C_ICMPV4);
+      if (plen == 8u) break;
+      if ((F.pl_raw & 15u) == D_PAYLOAD) put(GPD_C_PAYLOAD);
+      else stop = GPD_LT_PAYLOAD;
+      break;
+    }
     if (!((d4 == D_TCP && g == 1u) || (d4 == D_UDP && g == 2u))) return false;
     uint32_t hl;
     if (g == 1u) {  // tcp.go:229-314
@@ -1709,23 +1740,12 @@ static hipError_t launch_t(const KParams &P, hipStream_t stream, int num_cus) {
   const size_t lds = img + (size_t)wave_lds_bytes(STAGE, FAST) * WAVES + 64;  // + slack
   const uint64_t per_cu = (160u * 1024u) / lds;                       // resident workgroups per CU
   uint64_t blocks = (ntiles + WAVES - 1) / WAVES;
-  static const int rounds = getenv("GPD_ROUNDS") ? atoi(getenv("GPD_ROUNDS")) : 4;  // A/B only
-  const uint64_t cap = (uint64_t)num_cus * (per_cu ? per_cu : 1) * (rounds > 0 ? rounds : 4);
+  const uint64_t cap = (uint64_t)num_cus * (per_cu ? per_cu : 1) * kGridRounds;
   if (blocks > cap) blocks = cap;
   if (blocks == 0) return hipSuccess;
   hipLaunchKernelGGL((decode_kernel<STAGE, FAST, EXT, PAGES, SWZ, WAVES, CS, HASH, MINW>), dim3((unsigned)blocks),
                      dim3(64 * WAVES), lds, stream, P);
   return hipGetLastError();
-}
-
-// Diagnostic selector GPD_GEOM (A/B only): 0 = rotated windows, 1 = linear windows.
-static int geom() {
-  static int g = -1;
-  if (g < 0) {
-    const char *e = getenv("GPD_GEOM");
-    g = e ? atoi(e) : 0;
-  }
-  return g;
 }
 
 template <int STAGE, bool CS, bool HASH, int MINW, bool DEFER = false, bool RPFX = true>
@@ -1734,59 +1754,30 @@ static hipError_t launch_rs(const KParams &P, hipStream_t stream, int num_cus) {
   const size_t lds = ((P.image_words * 4u + 15u) & ~15u) + 4 * (size_t)rs_wave_lds_bytes(STAGE) + 64;
   const uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>((160u * 1024u) / lds, MINW));
   uint64_t blocks = (ntiles + 3) / 4;
-  static const int rounds = getenv("GPD_ROUNDS") ? atoi(getenv("GPD_ROUNDS")) : 4;  // A/B only
-  const uint64_t cap = (uint64_t)num_cus * per_cu * (rounds > 0 ? rounds : 4);  // rounds of resident workgroups
+  const uint64_t cap = (uint64_t)num_cus * per_cu * kGridRounds;  // rounds of resident workgroups
   if (blocks > cap) blocks = cap;
   if (blocks == 0) return hipSuccess;
   hipLaunchKernelGGL((rs_kernel<STAGE, CS, HASH, MINW, DEFER, RPFX>), dim3((unsigned)blocks), dim3(256), lds, stream, P);
   return hipGetLastError();
 }
 
-// Diagnostic selector GPD_RS_MINW (A/B only): waves per SIMD the register-staged kernel is
-// compiled for.
-static int rs_minw() {
-  static int w = -1;
-  if (w < 0) {
-    const char *e = getenv("GPD_RS_MINW");
-    w = e ? atoi(e) : 0;
-  }
-  return w;
-}
-
-// the fast kernel reads headers at any byte address: linear windows
+// The fast path: the register-staged loop (rs_kernel), its register bound setting the waves
+// per SIMD (VGPRs <= 512 / MINW): 4 for 4 KiB windows, 3 for 8 KiB — what LDS admits, no
+// spills.  The register-computed chunk prefix pays off for long frames only (IMIX -3 %); with
+// small frames (pcap records, VXLAN) its extra registers and code cost 1-2 %.
 template <bool CS, bool HASH>
 static hipError_t launch_fast(const KParams &P, hipStream_t stream, int num_cus) {
-  if (geom() == 3) {  // A/B: the LDS-DMA double-buffered loop
-    // Register budgets match what LDS admits: 4 KiB windows fit four 4-wave workgroups per
-    // CU (4 waves per SIMD, <= 128 VGPRs each), 8 KiB windows two (2 waves per SIMD).
-    if (P.stage == 4096)
-      return launch_t<4096, true, false, false, false, 4, CS, HASH, 4>(P, stream, num_cus);
-    return launch_t<8192, true, false, false, false, 4, CS, HASH, 2>(P, stream, num_cus);
-  }
-  // register-staged loop; the register bound sets the waves per SIMD (VGPRs <= 512 / MINW)
-  // (defaults: 4 waves per SIMD for 4 KiB windows, 3 for 8 KiB: what LDS admits, no spills)
-  const int w = rs_minw();
-  if (P.stage == 4096) {
-    if (w == 2) return launch_rs<4096, CS, HASH, 2>(P, stream, num_cus);
-    if (w == 3) return launch_rs<4096, CS, HASH, 3>(P, stream, num_cus);
-    if (w == 6) return launch_rs<4096, CS, HASH, 3, true>(P, stream, num_cus);  // A/B
-    return launch_rs<4096, CS, HASH, 4>(P, stream, num_cus);
-  }
-  if (w == 2) return launch_rs<8192, CS, HASH, 2>(P, stream, num_cus);
-  // The register-computed chunk prefix pays off for long frames only (IMIX -3 %); with small
-  // frames (pcap records, VXLAN) its extra registers and code cost 1-2 %.
+  if (P.stage == 4096) return launch_rs<4096, CS, HASH, 4>(P, stream, num_cus);
   if (P.options & kRegPrefix) return launch_rs<8192, CS, HASH, 3>(P, stream, num_cus);
   return launch_rs<8192, CS, HASH, 3, false, false>(P, stream, num_cus);
 }
 
+// The generic decoder over LDS windows (ext records, other first layers, PAGES tables): the
+// windows' 16-byte slots rotated (swizzled) against bank conflicts.
 template <bool EXT, bool PAGES>
 static hipError_t launch_s(const KParams &P, hipStream_t stream, int num_cus) {
-  const bool swz = geom() != 1;
-  if (P.stage == 4096)
-    return swz ? launch_t<4096, false, EXT, PAGES, true, 4>(P, stream, num_cus)
-               : launch_t<4096, false, EXT, PAGES, false, 4>(P, stream, num_cus);
-  return swz ? launch_t<8192, false, EXT, PAGES, true, 4>(P, stream, num_cus)
-             : launch_t<8192, false, EXT, PAGES, false, 4>(P, stream, num_cus);
+  if (P.stage == 4096) return launch_t<4096, false, EXT, PAGES, true, 4>(P, stream, num_cus);
+  return launch_t<8192, false, EXT, PAGES, true, 4>(P, stream, num_cus);
 }
 
 bool fast_eligible(const KParams &P) {

@@ -217,6 +217,7 @@ struct gpd_ctx {
     void *d = nullptr;
     size_t bytes = 0;
   } scratch[16];
+  gpd_tuning tune{0, -1, -1, 0};  // gpd_ctx_set_tuning (all automatic by default)
   bool timing = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
@@ -423,6 +424,18 @@ int gpd_ctx_destroy(gpd_ctx *ctx) {
   return GPD_OK;
 }
 
+int gpd_ctx_set_tuning(gpd_ctx *ctx, const gpd_tuning *t) {
+  if (!ctx) return set_err(GPD_ERR_INVALID, "gpd_ctx_set_tuning: null ctx");
+  const gpd_tuning automatic{0, -1, -1, 0};
+  if (!t) t = &automatic;
+  if (t->window_bytes != 0 && t->window_bytes != 4096 && t->window_bytes != 8192)
+    return set_err(GPD_ERR_INVALID, "gpd_ctx_set_tuning: window_bytes %u (0, 4096 or 8192)", t->window_bytes);
+  if (t->shift < -1 || t->shift > 1 || t->reg_prefix < -1 || t->reg_prefix > 1)
+    return set_err(GPD_ERR_INVALID, "gpd_ctx_set_tuning: shift / reg_prefix outside {-1, 0, 1}");
+  ctx->tune = *t;
+  return GPD_OK;
+}
+
 int gpd_ctx_set_timing(gpd_ctx *ctx, int enable) {
   if (!ctx) return set_err(GPD_ERR_INVALID, "gpd_ctx_set_timing: null ctx");
   HIP_TRY(hipSetDevice(ctx->device));
@@ -484,32 +497,22 @@ static int launch(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, hipS
   // LDS window per buffer: the smallest of 4/8 KiB that holds a typical 64-packet tile
   const uint64_t mean_slot = (in->data_len + in->n - 1) / in->n;
   P.stage = mean_slot * 64 <= 4096 ? 4096u : 8192u;
-  {  // A/B and tests only: force the window size (read per launch)
-    const char *st = getenv("GPD_STAGE");
-    if (st) P.stage = atoi(st) == 8192 ? 8192u : 4096u;
-  }
+  if (ctx->tune.window_bytes) P.stage = ctx->tune.window_bytes;
   P.first = ctx->first;
   P.decoders = ctx->decoders;
   P.options = ctx->options;
-  {  // streamed bytes and results use the nt cache policy (read once / written once);
-     // GPD_DIAG=<0..3> overrides the two bits for A/B runs only
-    static const char *d = getenv("GPD_DIAG");
-    P.options |= (d ? ((uint32_t)atoi(d) & 3u) : 3u) << 28;
-    // Window copies shifted so that network headers sit 16-byte aligned in LDS, for batches
-    // of small frames (mean slot <= 96 B: a window holds 40+ packets and the saved misaligned
-    // reads outweigh the shifted copy; with IMIX-sized frames they do not).  GPD_NOSHIFT=1
-    // turns it off and GPD_SHIFT=0/1 forces it either way (A/B runs and the parity tests,
-    // which cover both copies; read per launch).
-    const char *ns = getenv("GPD_NOSHIFT");
-    const char *fs = getenv("GPD_SHIFT");
-    bool shift = mean_slot <= 96 && !(ns && atoi(ns));
-    if (fs) shift = atoi(fs) != 0;
-    if (shift) P.options |= 1u << 27;
-    // long frames (mean slot > 160 B): 8 KiB windows whose chunk prefix sums are computed
-    // from the registers at commit (GPD_RPFX=0/1 forces it for A/B runs and the tests)
-    const char *rp = getenv("GPD_RPFX");
-    if (rp ? atoi(rp) != 0 : (mean_slot > 160 && !shift)) P.options |= 1u << 26;
-  }
+  // streamed bytes and results use the nt cache policy (read once / written once)
+  P.options |= 3u << 28;
+  // Window copies shifted so that network headers sit 16-byte aligned in LDS, for batches of
+  // small frames (mean slot <= 96 B: a window holds 40+ packets and the saved misaligned reads
+  // outweigh the shifted copy; with IMIX-sized frames they do not).  gpd_ctx_set_tuning can
+  // force either copy (the parity tests cover both).
+  const bool shift = ctx->tune.shift >= 0 ? ctx->tune.shift != 0 : mean_slot <= 96;
+  if (shift) P.options |= 1u << 27;
+  // long frames (mean slot > 160 B): 8 KiB windows whose chunk prefix sums are computed from
+  // the registers at commit
+  if (ctx->tune.reg_prefix >= 0 ? ctx->tune.reg_prefix != 0 : (mean_slot > 160 && !shift))
+    P.options |= 1u << 26;
   P.nstores = 2u + (out->net_hash != nullptr) + (out->tp_hash != nullptr) + (out->csum != nullptr) +
               (out->hdr_off != nullptr);
   if (gpd::fast_eligible(P)) {  // fallback list scratch for this stream, sized for one launch

@@ -230,7 +230,22 @@ class DecodingLayerParser:
         key = (self.device, self.first, self._mask, self.options)
         if self._ctx is None or self._ctx.key != key:
             self._ctx = _Ctx(self.device, self.first, self._mask, self.options, self._tables)
+            self._ctx.tuned = None
+        if self._ctx.tuned != self.Tuning:
+            self._apply_tuning()
         return self._ctx
+
+    # Engine tuning (gpd_ctx_set_tuning): staging choices that never change a result.
+    # Keys: window_bytes (0 auto / 4096 / 8192), shift and reg_prefix (-1 auto / 0 / 1).
+    Tuning: Optional[dict] = None
+
+    def _apply_tuning(self):
+        from ._lib import GpdTuning
+        t = dict(window_bytes=0, shift=-1, reg_prefix=-1)
+        t.update(self.Tuning or {})
+        g = GpdTuning(int(t["window_bytes"]), int(t["shift"]), int(t["reg_prefix"]), 0)
+        check(lib.gpd_ctx_set_tuning(self._ctx.h, C.byref(g)), "gpd_ctx_set_tuning")
+        self._ctx.tuned = dict(self.Tuning) if self.Tuning else None
 
     # --- decoding -----------------------------------------------------------------
     def decode_device(self, dbatch: DeviceBatch, dres: DeviceResult, stream=None) -> None:

@@ -29,6 +29,12 @@
  *
  * Every per-packet output is bit-exact with the reference decoder on the
  * same bytes; see DESIGN.md §Semantics for the definition of each output.
+ *
+ * Threading: a context is used by one host thread at a time, as a DecodingLayerParser is
+ * (it holds mutable layer state and is not goroutine-safe).  Calls on one context
+ * from two threads at once are not supported (its staging slots, per-stream fallback lists
+ * and tuning are unlocked); give each thread its own context.  Contexts are independent, and
+ * one context may launch on several streams from its one thread.
  */
 #ifndef GPD_H_
 #define GPD_H_
@@ -40,7 +46,8 @@
 extern "C" {
 #endif
 
-#define GPD_ABI_VERSION 3  /* 2: ICMPv4 + LLC, 12 objects, 224-B ext; 3: gpd_result.hdr_off */
+#define GPD_ABI_VERSION 4  /* 2: ICMPv4 + LLC, 12 objects, 224-B ext; 3: gpd_result.hdr_off;
+                              4: gpd_ctx_set_tuning */
 
 /* ---- gopacket LayerType numbers (layertypes.go:14-154, decode.go:105-116) ---- */
 #define GPD_LT_ZERO            0
@@ -300,6 +307,20 @@ int  gpd_sync(gpd_ctx *ctx, void *stream);
  * that stream around the launch (ms); -1 if not available.  Requires gpd_ctx_set_timing(1). */
 int  gpd_ctx_set_timing(gpd_ctx *ctx, int enable);
 float gpd_last_kernel_ms(gpd_ctx *ctx);
+
+/* Engine tuning of later launches on ctx.  None of these changes a result — every setting
+ * decodes every packet bit-exactly — only how the fast kernel stages packets; the defaults
+ * choose per batch from its mean frame slot.  Tests force each staging mode, and A/B
+ * measurements compare them; a NULL pointer restores the defaults. */
+typedef struct gpd_tuning {
+  uint32_t window_bytes;  /* LDS window per wave: 0 automatic, 4096 or 8192 */
+  int32_t  shift;         /* window copies shifted so network headers sit 16-B aligned in LDS:
+                             -1 automatic (mean slot <= 96 B), 0 off, 1 on */
+  int32_t  reg_prefix;    /* 8 KiB windows' chunk prefix sums from the registers at commit:
+                             -1 automatic (mean slot > 160 B), 0 off, 1 on */
+  int32_t  reserved;
+} gpd_tuning;
+int  gpd_ctx_set_tuning(gpd_ctx *ctx, const gpd_tuning *t);
 const char *gpd_last_error_string(void);
 
 #ifdef __cplusplus
