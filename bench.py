@@ -44,6 +44,10 @@ CONFIGS = {
              "5-tuple flow hashes, synthetic seed 0x5EED0003", 1 << 22),
     "vxlan": ("config4: 2^23 x 128 B Eth/IPv4/UDP/VXLAN/Eth/IPv4/TCP, inner flow keys, "
               "synthetic seed 0x5EED0004", 1 << 23),
+    "mixed": ("traffic mix (not a BASELINE config): 2^22 frames of TCP 64/576/1500, UDP 64, VXLAN, "
+              "ICMPv4 echo, IPv6/TCP, 802.3/LLC (fast kernel) and IPv4 options, fragments, IPv6 "
+              "hop-by-hop, cut TCP headers (12 %, generic decoder); every decoder registered, "
+              "synthetic seed 0x5EED0007", 1 << 22),
     "pcap64": ("config5 (per GPU): a pcap capture of 2^24 x 64 B Eth/IPv4/UDP records decoded in "
                "place (the capture bytes are the batch buffer: 16-B record headers interleaved), "
                "records indexed by the native pcap walker; synthetic seed 0x5EED0002", 1 << 24),
@@ -57,6 +61,8 @@ def make_batch(config: str, n: int, rank: int):
         return synth.make_udp64(n, 0x5EED0002 + seed_off)
     if config == "imix":
         return synth.make_imix(n, 0x5EED0003 + seed_off)
+    if config == "mixed":
+        return synth.make_traffic_mix(n, 0x5EED0007 + seed_off)
     if config == "pcap64":
         from gopacket_amd import pcap as NP
         return NP.synth_capture(synth.make_udp64(n, 0x5EED0002 + seed_off))
@@ -235,6 +241,32 @@ def bench_record36(parser, dev_batch, n, local, stream, out, args):
             "Mpackets_per_s": round(n / ms / 1e3, 1),
             "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "read_frac": round(rb / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+
+
+def bench_split(parser, dev_batch, dev_res, n, local, stream):
+    """The launch split in two (gpd_last_launch_split): how many packets the fast kernel left to
+    the generic list kernel (options, fragments, hop-by-hop, errors ...) and each kernel's
+    event-timed share of the launch (mean of 5)."""
+    import ctypes as C
+
+    import torch
+    from gopacket_amd._lib import check, lib
+    h = parser.ctx().h
+    check(lib.gpd_ctx_set_timing(h, 1), "gpd_ctx_set_timing")
+    fb, fast, lst = C.c_uint64(), C.c_float(), C.c_float()
+    rows = []
+    try:
+        for _ in range(5):
+            parser.decode_device(dev_batch, dev_res, stream)
+            check(lib.gpd_last_launch_split(h, C.byref(fb), C.byref(fast), C.byref(lst)),
+                  "gpd_last_launch_split")
+            rows.append((fb.value, fast.value, lst.value))
+    finally:
+        lib.gpd_ctx_set_timing(h, 0)
+    torch.cuda.synchronize(local)
+    return {"packets": int(rows[-1][0]), "fraction": round(rows[-1][0] / n, 5),
+            "fast_kernel_ms": round(float(np.mean([r[1] for r in rows])), 4),
+            "list_kernel_ms": round(float(np.mean([r[2] for r in rows])), 4)}
 
 
 def bench_flows(parser, dev_batch, n, args, stream, local):
@@ -802,6 +834,9 @@ def main():
     parser = P.NewDecodingLayerParser(L.LayerTypeEthernet, P.Ethernet(), P.Dot1Q(), P.IPv4(),
                                       P.IPv6(), P.IPv6ExtensionSkipper(), P.TCP(), P.UDP(),
                                       P.VXLAN(), P.Payload(), P.Fragment(), device=local)
+    if args.config == "mixed":  # the reference benchmark's set and more: ICMPv4 and LLC too
+        parser.AddDecodingLayer(P.ICMPv4())
+        parser.AddDecodingLayer(P.LLC())
     stream = torch.cuda.current_stream(local)
     if args.tune:
         parser.Tuning = {k: int(v) for k, v in (kv.split("=") for kv in args.tune.split(","))}
@@ -880,6 +915,7 @@ def main():
                     batch, n_err, interleaved=16 if pcap_info else 0)
     if not args.ablate:  # the 36-B record (hdr_off on, as the flow table consumes it)
         out["record36"] = bench_record36(parser, dev_batch, n, local, stream, out, args)
+        out["fallback"] = bench_split(parser, dev_batch, dev_res, n, local, stream)
     if pcap_info:
         out["pcap"] = pcap_info
         if args.replay:

@@ -56,6 +56,8 @@ EXPORTS = {
     "gpd_ctx_set_timing": (C.c_int, [C.c_void_p, C.c_int]),
     "gpd_last_kernel_ms": (C.c_float, [C.c_void_p]),
     "gpd_ctx_set_tuning": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "gpd_last_launch_split": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_float),
+                                        C.POINTER(C.c_float)]),
     "gpd_last_error_string": (C.c_char_p, []),
     # include/gpd_pcap.h
     "gpd_pcap_header": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(GpdPcapInfo)]),

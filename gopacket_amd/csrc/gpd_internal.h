@@ -83,8 +83,9 @@ bool fast_eligible(const KParams &P);
 // One launch covers at most this many packets, so packet and tile indices are 32-bit.
 constexpr uint64_t kMaxLaunchPackets = 1ull << 30;
 
-// Launch the decode kernel over P (asynchronous on `stream`).
-hipError_t launch_decode(const KParams &P, hipStream_t stream, int num_cus);
+// Launch the decode kernel over P (asynchronous on `stream`).  `mid` (may be null) is
+// recorded between the fast kernel and the list kernel of the fallback packets.
+hipError_t launch_decode(const KParams &P, hipStream_t stream, int num_cus, hipEvent_t mid = nullptr);
 
 // Host side: set the thread's gpd_last_error_string() text and return `code` (gpd_runtime.cpp).
 int set_error(int code, const char *fmt, ...);

@@ -1786,7 +1786,7 @@ bool fast_eligible(const KParams &P) {
          (P.decoders & GPD_DEC_ETHERNET);
 }
 
-hipError_t launch_decode(const KParams &P, hipStream_t stream, int num_cus) {
+hipError_t launch_decode(const KParams &P, hipStream_t stream, int num_cus, hipEvent_t mid) {
   if (P.n > kMaxLaunchPackets) return hipErrorInvalidValue;
   if (fast_eligible(P)) {
     if (!P.fb_count || !P.fb_next || !P.fb_list) return hipErrorInvalidValue;
@@ -1797,6 +1797,7 @@ hipError_t launch_decode(const KParams &P, hipStream_t stream, int num_cus) {
            : (hash ? launch_fast<false, true>(P, stream, num_cus)
                    : launch_fast<false, false>(P, stream, num_cus));
     if (e != hipSuccess) return e;
+    if (mid && (e = hipEventRecord(mid, stream)) != hipSuccess) return e;
     const size_t lds = (P.image_words * 4u + 15u) & ~15u;
     hipLaunchKernelGGL(list_kernel<false>, dim3((unsigned)num_cus * 2), dim3(256), lds, stream, P);
     return hipGetLastError();

@@ -219,8 +219,10 @@ struct gpd_ctx {
   } scratch[16];
   gpd_tuning tune{0, -1, -1, 0};  // gpd_ctx_set_tuning (all automatic by default)
   bool timing = false;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, evm = nullptr;
   bool timed = false;
+  bool timed_split = false;           // evm marks the fast kernel's end in the timed launch
+  uint32_t *timed_fb_count = nullptr;  // its fallback counter (device)
   // gpd_decode_host staging (two slots)
   struct Slot {
     hipStream_t stream = nullptr;
@@ -420,7 +422,24 @@ int gpd_ctx_destroy(gpd_ctx *ctx) {
   for (const auto &r : ctx->registered) (void)hipHostUnregister((void *)r.first);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+  if (ctx->evm) (void)hipEventDestroy(ctx->evm);
   delete ctx;
+  return GPD_OK;
+}
+
+int gpd_last_launch_split(gpd_ctx *ctx, uint64_t *fallback, float *fast_ms, float *list_ms) {
+  if (!ctx || !fallback || !fast_ms || !list_ms)
+    return set_err(GPD_ERR_INVALID, "gpd_last_launch_split: null argument");
+  if (!ctx->timed || !ctx->timed_split)
+    return set_err(GPD_ERR_INVALID, "gpd_last_launch_split: no timed fast-path launch "
+                                    "(gpd_ctx_set_timing(1), then one gpd_decode of <= 2^30 packets)");
+  HIP_TRY(hipSetDevice(ctx->device));
+  HIP_TRY(hipEventSynchronize(ctx->ev1));
+  HIP_TRY(hipEventElapsedTime(fast_ms, ctx->ev0, ctx->evm));
+  HIP_TRY(hipEventElapsedTime(list_ms, ctx->evm, ctx->ev1));
+  uint32_t c = 0;  // the launch's counter stays until the launch after next zeroes it
+  HIP_TRY(hipMemcpy(&c, ctx->timed_fb_count, sizeof c, hipMemcpyDeviceToHost));
+  *fallback = c;
   return GPD_OK;
 }
 
@@ -442,6 +461,7 @@ int gpd_ctx_set_timing(gpd_ctx *ctx, int enable) {
   if (enable && !ctx->ev0) {
     HIP_TRY(hipEventCreate(&ctx->ev0));
     HIP_TRY(hipEventCreate(&ctx->ev1));
+    HIP_TRY(hipEventCreate(&ctx->evm));
   }
   ctx->timing = enable != 0;
   ctx->timed = false;
@@ -533,6 +553,8 @@ static int launch(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, hipS
     P.fb_list = fb.d + 128;
   }
   if (record) HIP_TRY(hipEventRecord(ctx->ev0, stream));
+  const bool split = record && in->n <= gpd::kMaxLaunchPackets && gpd::fast_eligible(P);
+  ctx->timed_split = false;
   // launches of <= kMaxLaunchPackets packets keep every packet/tile index 32-bit in the kernel
   for (uint64_t lo = 0; lo < in->n; lo += gpd::kMaxLaunchPackets) {
     gpd::KParams Q = P;
@@ -552,12 +574,14 @@ static int launch(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, hipS
       Q.fb_next = fb.d + 64 * (fb.parity ^ 1u);
       fb.parity ^= 1u;
     }
-    hipError_t e = gpd::launch_decode(Q, stream, ctx->num_cus);
+    hipError_t e = gpd::launch_decode(Q, stream, ctx->num_cus, split ? ctx->evm : nullptr);
     if (e != hipSuccess) return set_err(GPD_ERR_HIP, "decode kernel launch: %s", hipGetErrorString(e));
+    if (split) ctx->timed_fb_count = Q.fb_count;
   }
   if (record) {
     HIP_TRY(hipEventRecord(ctx->ev1, stream));
     ctx->timed = true;
+    ctx->timed_split = split;
   }
   return GPD_OK;
 }

@@ -290,6 +290,127 @@ def make_vxlan(n: int, seed: int = 0x5EED0004) -> PacketBatch:
                        np.full(n, 128, dtype=np.uint32))
 
 
+# ---- a traffic mix with the rarer stacks and the generic decoder's share -------------------
+# (class, frame bytes, weight in 100): what the fast kernel decodes itself, then what it leaves
+# to the generic decoder (IPv4 options, fragments, IPv6 hop-by-hop, a TCP header cut short)
+MIX_CLASSES = (("tcp64", 64, 30), ("tcp576", 576, 15), ("tcp1500", 1500, 8), ("udp64", 64, 20),
+               ("vxlan", 128, 5), ("icmp4", 98, 5), ("tcp6", 86, 5), ("stp", 60, 1),
+               ("ip4opt", 68, 4), ("frag", 64, 3), ("ip6hbh", 90, 2), ("tcpcut", 64, 2))
+MIX_FALLBACK = ("ip4opt", "frag", "ip6hbh", "tcpcut")
+
+
+def _mix_class(name: str, m: int, seed: int, free_t, free_u) -> np.ndarray:
+    """m frames of one traffic-mix class (rows of the class's frame size)."""
+    r = [splitmix64(seed, m, k) for k in range(8)]
+    if name.startswith("tcp") and name != "tcp6" and name != "tcpcut":
+        return _tcp_frames(m, int(name[3:]), r, np.zeros(0, np.int64), False, free_t,
+                           np.nonzero((np.arange(m) % 64) == 63)[0], seed, 300)
+    if name == "tcpcut":  # a 64-B TCP frame captured to 50 B: the header is cut (tcp.go:264-265)
+        return _tcp_frames(m, 64, r, np.zeros(0, np.int64), False, free_t, np.zeros(0, np.int64),
+                           seed, 302)
+    if name in ("udp64", "frag", "ip4opt"):
+        a = np.zeros((m, 64), np.uint8)
+        _udp64_rows(a, seed, 0, free_u)
+        if name == "frag":  # More Fragments set: next layer Fragment (ip4.go:281-286)
+            a[:, 20] = 0x20
+            a[:, 24:26] = 0
+            _be16(a, 24, _fold_not(_sum16(a[:, 14:34])))
+            return a
+        if name == "ip4opt":  # IHL 6: Router Alert (RFC 2113), options walk (ip4.go:240-273)
+            b = np.zeros((m, 68), np.uint8)
+            b[:, :34] = a[:, :34]
+            b[:, 34:38] = np.array([0x94, 0x04, 0, 0], np.uint8)
+            b[:, 38:] = a[:, 34:]
+            b[:, 14] = 0x46
+            _be16(b, 16, np.full(m, 54))
+            b[:, 24:26] = 0
+            _be16(b, 24, _fold_not(_sum16(b[:, 14:38])))
+            return b
+        return a
+    if name == "vxlan":
+        return make_vxlan(m, seed).data[:m * 128].reshape(m, 128)
+    if name == "icmp4":  # echo request with 56 bytes of data (icmp4.go:220-231)
+        a = np.zeros((m, 98), np.uint8)
+        a[:, 0:12] = _rand_bytes(seed, 110, m, 12) & 0xFE
+        _be16(a, 12, np.full(m, 0x0800))
+        _ip4_header(a, 14, np.full(m, 84), (r[1] & np.uint64(0xFFFF)).astype(np.int64),
+                    np.full(m, 64, np.uint8), 1, r[2] & np.uint64(0xFFFFFFFF), r[2] >> np.uint64(32))
+        a[:, 34] = 8
+        _be16(a, 38, (r[3] & np.uint64(0xFFFF)).astype(np.int64))
+        _be16(a, 40, ((r[3] >> np.uint64(16)) & np.uint64(0xFFFF)).astype(np.int64))
+        a[:, 42:98] = _rand_bytes(seed, 111, m, 56)
+        _be16(a, 36, _fold_not(_sum16(a[:, 34:98])))
+        return a
+    if name in ("tcp6", "ip6hbh"):
+        size = 86 if name == "tcp6" else 90
+        a = np.zeros((m, size), np.uint8)
+        a[:, 0:12] = _rand_bytes(seed, 112, m, 12) & 0xFE
+        _be16(a, 12, np.full(m, 0x86DD))
+        a[:, 14] = 0x60
+        a[:, 21] = 64
+        a[:, 22:54] = _rand_bytes(seed, 113, m, 32)
+        if name == "tcp6":  # IPv6 / TCP, 12 bytes of payload
+            _be16(a, 18, np.full(m, 32))
+            a[:, 20] = 6
+            _be16(a, 54, _pick(free_t, r[4]))
+            _be16(a, 56, _pick(free_t, r[4] >> np.uint64(32)))
+            a[:, 66] = 0x50
+            a[:, 67] = 0x18
+            _be16(a, 68, np.full(m, 0x2000))
+            a[:, 74:86] = _rand_bytes(seed, 114, m, 12)
+            a[:, 70:72] = 0
+            s = _sum16(a[:, 22:54]) + np.uint64(6) + np.uint64(32) + _sum16(a[:, 54:86])
+            _be16(a, 70, _fold_not(s))
+            return a
+        # IPv6 / hop-by-hop (Router Alert for MLD) / ICMPv6: HBH parsed inside IPv6 (ip6.go:509-526)
+        _be16(a, 18, np.full(m, 36))
+        a[:, 20] = 0
+        a[:, 54:62] = np.array([58, 0, 5, 2, 0, 0, 1, 0], np.uint8)
+        a[:, 62] = 143
+        a[:, 66:90] = _rand_bytes(seed, 115, m, 24)
+        return a
+    if name == "stp":  # 802.3 length 38, LLC 42/42/03, a spanning-tree BPDU (llc.go:31-69)
+        a = np.zeros((m, 60), np.uint8)
+        a[:, 0:6] = np.array([0x01, 0x80, 0xC2, 0, 0, 0], np.uint8)
+        a[:, 6:12] = _rand_bytes(seed, 116, m, 6) & 0xFE
+        _be16(a, 12, np.full(m, 38))
+        a[:, 14:17] = np.array([0x42, 0x42, 0x03], np.uint8)
+        a[:, 17:52] = _rand_bytes(seed, 117, m, 35)
+        return a
+    raise ValueError(name)
+
+
+def make_traffic_mix(n: int, seed: int = 0x5EED0007, align: int = 16) -> PacketBatch:
+    """A seeded mix of MIX_CLASSES by weight, shuffled: TCP 64/576/1500, UDP 64, VXLAN, ICMPv4
+    echo, IPv6/TCP and 802.3/LLC frames that the fast kernel decodes, plus IPv4 options, IPv4
+    fragments, IPv6 hop-by-hop and cut TCP headers (12 %) that it leaves to the generic
+    decoder.  Checksums are valid except 1 in 64 TCP frames."""
+    wsum = sum(w for _, _, w in MIX_CLASSES)
+    counts = [n * w // wsum for _, _, w in MIX_CLASSES]
+    counts[0] += n - sum(counts)
+    cls = np.repeat(np.arange(len(MIX_CLASSES)), counts)
+    cls = cls[np.argsort(splitmix64(seed, n, 97), kind="stable")]
+    sizes = np.array([sz for _, sz, _ in MIX_CLASSES], np.int64)[cls]
+    slot = (sizes + align - 1) // align * align
+    offs = np.zeros(n, np.int64)
+    if n > 1:
+        np.cumsum(slot[:-1], out=offs[1:])
+    total = int(offs[-1] + sizes[-1]) if n else 0
+    data = np.zeros(total + PAD, np.uint8)
+    free_t, free_u = _free_ports(TABLES.tcp_port), _free_ports(TABLES.udp_port)
+    caplen = sizes.copy()
+    for k, (name, size, _) in enumerate(MIX_CLASSES):
+        rows = np.nonzero(cls == k)[0]
+        if not len(rows):
+            continue
+        frames = _mix_class(name, len(rows), seed + 1000 * (k + 1), free_t, free_u)
+        idx = offs[rows][:, None] + np.arange(size)[None, :]
+        data[idx.reshape(-1)] = frames.reshape(-1)
+        if name == "tcpcut":
+            caplen[rows] = 50
+    return PacketBatch(data, total, offs.astype(np.uint32), caplen.astype(np.uint32))
+
+
 def make_mixed(n: int, seed: int = 0x5EED0005) -> PacketBatch:
     """A mixed batch (the three configurations interleaved) for parity tests."""
     parts = [make_udp64(n // 3 + 1, seed), make_imix(n // 3 + 1, seed + 1), make_vxlan(n // 3 + 1, seed + 2)]

@@ -307,6 +307,11 @@ int  gpd_sync(gpd_ctx *ctx, void *stream);
  * that stream around the launch (ms); -1 if not available.  Requires gpd_ctx_set_timing(1). */
 int  gpd_ctx_set_timing(gpd_ctx *ctx, int enable);
 float gpd_last_kernel_ms(gpd_ctx *ctx);
+/* The last timed gpd_decode split in two (synchronises its stream): the packets the fast
+ * kernel left to the generic decoder (options, fragments, hop-by-hop, errors, ...), the fast
+ * kernel's time and the generic list kernel's time (ms).  Needs a timed launch that took the
+ * fast path (Ethernet first, hashed tables, no ext records). */
+int  gpd_last_launch_split(gpd_ctx *ctx, uint64_t *fallback, float *fast_ms, float *list_ms);
 
 /* Engine tuning of later launches on ctx.  None of these changes a result — every setting
  * decodes every packet bit-exactly — only how the fast kernel stages packets; the defaults

@@ -351,3 +351,35 @@ def test_full_size_config4_vxlan_properties():
     assert int(res.net_hash[0]) == int(ref0.net_hash[0]) and int(res.tp_hash[0]) == int(ref0.tp_hash[0])
     del res
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("mask", [ALL, 0x3FF])
+def test_traffic_mix_both_kernels(mask):
+    """The traffic mix (ICMPv4 echo, 802.3/LLC, IPv6/TCP, VXLAN, TCP/UDP, and the generic
+    decoder's share: IPv4 options, fragments, IPv6 hop-by-hop, cut TCP headers) with every
+    decoder registered and without ICMPv4/LLC (they then stop as unsupported)."""
+    run_both(synth.make_traffic_mix(1 << 15), mask=mask, ext=True)
+    run_both(synth.make_traffic_mix(1 << 15, seed=9), mask=mask, options=1, ext=False)
+
+
+def test_fallback_split_counts_the_generic_share():
+    """gpd_last_launch_split: the fast kernel decodes ICMPv4, LLC, IPv6/TCP and VXLAN itself,
+    and leaves exactly the IPv4-options, fragment, hop-by-hop and cut-TCP frames to the list
+    kernel."""
+    import ctypes as C
+    from gopacket_amd import parser as P
+    from gopacket_amd._lib import check, lib
+    n = 1 << 16
+    b = synth.make_traffic_mix(n)
+    p = P.DecodingLayerParser(L.LayerTypeEthernet)
+    p._mask = ALL
+    db, dr = P.DeviceBatch(b, 0), P.DeviceResult(n, 0)
+    h = p.ctx().h
+    check(lib.gpd_ctx_set_timing(h, 1), "timing")
+    p.decode_device(db, dr)
+    fb, f, l = C.c_uint64(), C.c_float(), C.c_float()
+    check(lib.gpd_last_launch_split(h, C.byref(fb), C.byref(f), C.byref(l)), "split")
+    wsum = sum(w for _, _, w in synth.MIX_CLASSES)
+    want = sum(n * w // wsum for name, _, w in synth.MIX_CLASSES if name in synth.MIX_FALLBACK)
+    assert fb.value == want and f.value > 0 and l.value > 0
+    lib.gpd_ctx_set_timing(h, 0)
