@@ -278,6 +278,25 @@ case("udp6_dstopts_checksum_kat", v6 + dst + udp,
      "layers/tcpip_test.go:17,95-137 (Wireshark-confirmed 0x4d21; DstOpts with one PadN(4) option)",
      first="IPv6")
 
+# IPv6 destination options (ip6_test.go): IPv6Destination has DecodeFromBytes but no CanDecode /
+# NextLayerType (ip6.go:633-667), so it is not a DecodingLayer; a DLP reaches it through
+# IPv6ExtensionSkipper (CanDecode LayerClassIPv6Extension, layertypes.go:193-198)
+p = go_bytes_at("layers/ip6_test.go", "var testPacketIPv6Destination0")
+src = f"layers/ip6_test.go:{line_of('layers/ip6_test.go', 'var testPacketIPv6Destination0')}"
+case("ipv6_destination0", p, src, ["IPv6", "IPv6ExtensionSkipper", "Payload"],
+     {"decoded": ["IPv6", "IPv6Destination"], "err": None, "truncated": False,
+      "ipv6": {"contents": [0, 40], "payload": [40, 48]}},
+     "layers/ip6_test.go:244-300 (checkLayers [IPv6 IPv6Destination]; IPv6 Length 8, NextHeader "
+     "60, HopLimit 64; the destination header's Contents = bytes 40..48, NextHeader NoNextHeader, "
+     "empty Payload); DLP: the skipper consumes the header (ip6.go:443-461), next = Payload "
+     "(enums.go IPProtocolNoNextHeader), and the empty payload ends the loop "
+     "(layers_decoder.go:71-73)", first="IPv6")
+case("ipv6_destination0_unregistered", p, src, ["IPv6", "Payload"],
+     {"decoded": ["IPv6"], "err": "No decoder for layer type IPv6Destination", "stop": 49,
+      "truncated": False},
+     "derived: without IPv6ExtensionSkipper the loop stops at LayerTypeIPv6Destination "
+     "(parser.go:308-314)", first="IPv6")
+
 # 15. ICMPv4 and LLC decoders
 p = go_bytes_at("layers/vxlan_test.go", "var testPacketVXLAN")
 src = f"layers/vxlan_test.go:{line_of('layers/vxlan_test.go', 'var testPacketVXLAN')}"
