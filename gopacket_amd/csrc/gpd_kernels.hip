@@ -617,7 +617,6 @@ done:
 // Straight-line decode of the stacks that carry nearly all traffic:
 //   Ethernet [Dot1Q]{0,2} (IPv4 with IHL 5 | IPv6 without hop-by-hop) (TCP | UDP | ICMPv4)
 //     [Payload | VXLAN + the same stack once more]
-//   Ethernet (802.3 length) LLC (SNAP / STP unsupported, or nothing)
 // for a packet in an LDS window, with Ethernet as the first layer.  Header offsets are
 // runtime values and every header is read straight from LDS at its own byte address
 // (gfx950 DS instructions take unaligned addresses), so one code path serves every tag
@@ -820,7 +819,7 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
     uint32_t W[16];
     load64(W, p + b + 14);
     const uint32_t et0 = be_lo(e.y), et1 = be_lo(e.z), et2 = be_lo(e.w);
-    const bool llc = et0 < 0x0600u;  // 802.3 length framing: EthernetTypeLLC (0)
+    if (et0 < 0x0600u) return false;  // 802.3 length framing (LLC): the generic decoder
     const uint32_t t1 = tag_type(et0), t2 = t1 & tag_type(et1);
     const uint32_t l3 = b + 14 + 4 * (t1 + t2);
     if (t1) load64(W, p + l3);  // tagged: the network header is further in
@@ -839,7 +838,7 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
     const uint32_t ulen = be_lo(ty);
     const uint32_t seg = (g == 2u && ulen >= 8u && ulen <= plen) ? ulen : plen;
     // ---- round trip 2: all lookups
-    const uint32_t r0 = fix_bucket<kFixEthBase>(F.mult, llc ? 0u : et0);
+    const uint32_t r0 = fix_bucket<kFixEthBase>(F.mult, et0);
     uint32_t r1 = 0, r2 = 0;
     if (t1) {
       r1 = fix_bucket<kFixEthBase>(F.mult, et1);
@@ -851,27 +850,6 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
     const uint32_t rs = fix_bucket_at(pbase, F.mult, be_lo(tx));
     // ---- Ethernet / Dot1Q (dot1q.go:29-50), confirming the tag guesses
     put(GPD_C_ETHERNET);
-    if (llc) {  // ethernet.go:50-57: the EtherType field is the payload length
-      uint32_t pl = lim - b - 14u;
-      if (pl < et0) trunc = 1;
-      else pl = et0;
-      const uint32_t d0 = r0 & 15u;
-      if (pl == 0) break;  // empty payload: the loop stops (layers_decoder.go:71-73)
-      if (d0 == D_NONE) { stop = (r0 >> 8) & 0xFFu; break; }
-      if (d0 != D_LLC || pl < 3u) return false;  // remapped, or "LLC header too small"
-      // LLC, llc.go:31-52: DSAP / SSAP without their low bits, a one- or two-byte control
-      const uint32_t dsap = (e.y >> 16) & 0xFEu, ssap = (e.y >> 24) & 0xFEu, ctl = e.z & 0xFFu;
-      const uint32_t cl = (!(ctl & 1u) || (ctl & 3u) == 1u) ? 4u : 3u;
-      if (pl < cl) return false;
-      put(GPD_C_LLC);
-      if (pl == cl) break;
-      // NextLayerType, llc.go:61-69: SNAP, STP or Zero (a lookup of Zero misses: nil error)
-      const uint32_t nt = (dsap == 0xAAu && ssap == 0xAAu) ? (uint32_t)GPD_LT_SNAP
-                        : (dsap == 0x42u && ssap == 0x42u) ? (uint32_t)GPD_LT_STP : 0u;
-      if (nt && (g_lds[nt] & 15u) != D_NONE) return false;
-      stop = nt;
-      break;
-    }
     if (((r0 & 15u) == D_DOT1Q) != (t1 != 0)) return false;
     uint32_t r = r0;
     if (t1) {
