@@ -132,6 +132,11 @@ func (p *BatchDecodingLayerParser) ReloadTables(t *Tables) error {
 		tcp_port:    (*C.uint16_t)(unsafe.Pointer(&t.TCPPort[0])),
 		udp_port:    (*C.uint16_t)(unsafe.Pointer(&t.UDPPort[0])),
 	}
+	// cfg (Go memory) holds pointers into the four Go slices: cgo lets C see them only while
+	// they are pinned (runtime.Pinner, Go 1.21+)
+	var pn runtime.Pinner
+	defer pn.Unpin()
+	pinFirst(&pn, t.EtherType, t.IPProtocol, t.TCPPort, t.UDPPort)
 	if rc := C.gpd_ctx_reload_tables(p.ctx, &cfg); rc != C.GPD_OK {
 		return lastError("gpd_ctx_reload_tables", rc)
 	}
@@ -216,22 +221,52 @@ func (p *BatchDecodingLayerParser) DecodeBatch(b *PacketBatch) (*Result, error) 
 		caplen:   (*C.uint32_t)(unsafe.Pointer(&b.CapLen[0])),
 		n:        C.uint64_t(n),
 	}
-	out := C.gpd_result{
-		status:   (*C.uint32_t)(unsafe.Pointer(&r.Status[0])),
-		layers:   (*C.uint64_t)(unsafe.Pointer(&r.Layers[0])),
-		net_hash: (*C.uint64_t)(unsafe.Pointer(&r.NetHash[0])),
-		tp_hash:  (*C.uint64_t)(unsafe.Pointer(&r.TpHash[0])),
-		csum:     (*C.uint32_t)(unsafe.Pointer(&r.Checksum[0])),
-		hdr_off:  (*C.uint32_t)(unsafe.Pointer(&r.HdrOff[0])),
-	}
+	out := r.cResult()
 	if err := p.configure(); err != nil {
 		return nil, err
 	}
+	// in and out (Go memory) hold pointers into Go slices: pinned for the call
+	var pn runtime.Pinner
+	defer pn.Unpin()
+	pinFirst(&pn, data, b.Offset, b.CapLen)
+	r.pin(&pn)
 	if rc := C.gpd_decode_host(p.ctx, &in, &out); rc != C.GPD_OK {
 		return nil, lastError("gpd_decode_host", rc)
 	}
-	runtime.KeepAlive(data)
 	return r, nil
+}
+
+// pinFirst pins the backing array of every non-empty slice (its first element): a C struct
+// in Go memory may hold pointers into Go memory only while they are pinned (cgo pointer
+// rules; runtime.Pinner, Go 1.21+).  Slices over memory Go does not own (an mmap'ed ring or
+// capture) must not be passed: Pin accepts Go pointers only.
+func pinFirst(pn *runtime.Pinner, slices ...interface{}) {
+	for _, s := range slices {
+		switch v := s.(type) {
+		case []byte:
+			if len(v) > 0 {
+				pn.Pin(&v[0])
+			}
+		case []uint16:
+			if len(v) > 0 {
+				pn.Pin(&v[0])
+			}
+		case []uint32:
+			if len(v) > 0 {
+				pn.Pin(&v[0])
+			}
+		case []uint64:
+			if len(v) > 0 {
+				pn.Pin(&v[0])
+			}
+		case []int32:
+			if len(v) > 0 {
+				pn.Pin(&v[0])
+			}
+		default:
+			panic("gpdecode: pinFirst: unsupported slice type")
+		}
+	}
 }
 
 // configure re-creates the context when the parser options changed.

@@ -75,6 +75,9 @@ func (p *BatchDecodingLayerParser) DecodeCapture(capture []byte, maxPackets int)
 	}
 	r = newResult(maxPackets)
 	out := r.cResult()
+	var pn runtime.Pinner // out (Go memory) points into r's slices
+	defer pn.Unpin()
+	r.pin(&pn)
 	var n, pos C.uint64_t
 	var stop C.int
 	rc := C.gpd_decode_pcap(p.ctx, (*C.uint8_t)(unsafe.Pointer(&capture[0])), C.uint64_t(len(capture)),
@@ -139,6 +142,12 @@ func (p *BatchDecodingLayerParser) DecodeRing(ring *Ring, maxPackets int, addVLA
 		vlan:     (*C.int32_t)(unsafe.Pointer(&pk.VLAN[0])),
 	}
 	out := r.cResult()
+	// out and cpk (Go memory) point into Go slices: pinned for the call; ring.Mem is the
+	// mmap'ed ring (not Go memory), which cgo passes as it is
+	var pn runtime.Pinner
+	defer pn.Unpin()
+	r.pin(&pn)
+	pinFirst(&pn, pk.Offset, pk.CapLen, pk.Length, pk.Timestamp, pk.IfIndex, pk.VLAN)
 	add := C.int(0)
 	if addVLANHeader {
 		add = 1
@@ -358,6 +367,11 @@ func (r *Result) cResult() C.gpd_result {
 		csum:     (*C.uint32_t)(unsafe.Pointer(&r.Checksum[0])),
 		hdr_off:  (*C.uint32_t)(unsafe.Pointer(&r.HdrOff[0])),
 	}
+}
+
+// pin pins r's arrays (the ones cResult points a gpd_result at) until pn.Unpin.
+func (r *Result) pin(pn *runtime.Pinner) {
+	pinFirst(pn, r.Status, r.Layers, r.NetHash, r.TpHash, r.Checksum, r.HdrOff)
 }
 
 func (r *Result) truncate(n int) {

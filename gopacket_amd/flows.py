@@ -186,6 +186,9 @@ class ShardedFlowTable:
             recv, rcv = keys[:m], send
         else:
             recv, rcv = exchange_keys(keys[:m], send, self.group)
+            # the collective completes on torch's current stream; a caller's own stream must
+            # wait for it before the insert reads the received records
+            self._after_collective(stream, dev)
         t2 = time.perf_counter()
         ids = torch.empty(max(recv.shape[0], 1), dtype=torch.int32, device=dev)
         check(lib.gpd_flow_insert_keys(t.h, C.c_void_p(recv.data_ptr()), int(recv.shape[0]),
@@ -195,7 +198,11 @@ class ShardedFlowTable:
             stream.synchronize()
         torch.cuda.synchronize(dev)
         t3 = time.perf_counter()
-        back = ids[:m] if self.single else return_ids(ids[:recv.shape[0]], rcv, send, self.group)
+        if self.single:
+            back = ids[:m]
+        else:
+            back = return_ids(ids[:recv.shape[0]], rcv, send, self.group)
+            self._after_collective(stream, dev)
         owner = torch.empty(dbatch.n, dtype=torch.int32, device=dev)
         flow_id = torch.empty(dbatch.n, dtype=torch.int32, device=dev)
         check(lib.gpd_flow_key_ids(t.h, C.c_void_p(keys.data_ptr()), m, C.c_void_p(back.data_ptr()),
@@ -206,6 +213,14 @@ class ShardedFlowTable:
         self.last_ms = {"keys": (t1 - t0) * 1e3, "exchange": (t2 - t1) * 1e3,
                         "insert": (t3 - t2) * 1e3, "return": (t4 - t3) * 1e3}
         return owner, flow_id
+
+    @staticmethod
+    def _after_collective(stream, dev):
+        if stream is not None:
+            torch = _torch()
+            cur = torch.cuda.current_stream(dev)
+            if stream != cur:
+                stream.wait_stream(cur)
 
     def Stats(self, stream=None) -> dict:
         return self.table.Stats(stream)
