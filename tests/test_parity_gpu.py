@@ -383,3 +383,26 @@ def test_fallback_split_counts_the_generic_share():
     want = sum(n * w // wsum for name, _, w in synth.MIX_CLASSES if name in synth.MIX_FALLBACK)
     assert fb.value == want and f.value > 0 and l.value > 0
     lib.gpd_ctx_set_timing(h, 0)
+
+
+def test_host_path_recovers_after_a_failed_call():
+    """gpd_decode_host fails on a packet no staging slot holds (> 256 MB) after earlier chunks
+    were already in flight; the next call on the same context must start from idle slots and
+    decode its own batch exactly (no stale chunk drained into its results)."""
+    from gopacket_amd import parser as P
+    from gopacket_amd._lib import GpdError
+    small = synth.make_udp64(3 * (1 << 20) // 2)  # two chunks in flight before the big one
+    big = (257 << 20)
+    data = np.zeros(small.data_len + big + 64, np.uint8)
+    data[:small.data_len] = small.data[:small.data_len]
+    off = np.concatenate([small.offset, [small.data_len]]).astype(np.uint32)
+    cap = np.concatenate([small.caplen, [big]]).astype(np.uint32)
+    bad = PacketBatch(data, small.data_len + big, off, cap)
+    p = P.DecodingLayerParser(L.LayerTypeEthernet)
+    p._mask = ALL
+    with pytest.raises(GpdError, match="larger than"):
+        p.DecodeBatchHost(bad)
+    del data, bad
+    nxt = synth.make_mixed(5000, seed=0x77)
+    ref = O.decode(nxt, L.LayerTypeEthernet, ALL, 0, ext=False, nthreads=8)
+    assert_same(p.DecodeBatchHost(nxt), ref, nxt, ext=False)
