@@ -71,6 +71,7 @@ struct KParams {
   uint32_t stage;              // LDS window bytes per buffer (chosen by the runtime)
   uint32_t nstores;            // store instructions per tile (non-NULL result arrays)
   uint32_t fixed;              // tables in the kFix* layout (eth_mult shared by all three)
+  uint32_t waves;              // fast kernel waves per SIMD (0: the default for the window)
   uint32_t *fb_count;          // fast kernel: fallback list length (device scratch, zero)
   uint32_t *fb_next;           // the counter the next fast launch uses (list_kernel zeroes it)
   uint32_t *fb_list;           // fast kernel: packet indices left to the generic decoder

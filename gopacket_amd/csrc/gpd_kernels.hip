@@ -1745,7 +1745,12 @@ static hipError_t launch_rs(const KParams &P, hipStream_t stream, int num_cus) {
 // small frames (pcap records, VXLAN) its extra registers and code cost 1-2 %.
 template <bool CS, bool HASH>
 static hipError_t launch_fast(const KParams &P, hipStream_t stream, int num_cus) {
-  if (P.stage == 4096) return launch_rs<4096, CS, HASH, 4>(P, stream, num_cus);
+  if (P.stage == 4096) {
+    if (P.waves == 2) return launch_rs<4096, CS, HASH, 2>(P, stream, num_cus);
+    if (P.waves == 3) return launch_rs<4096, CS, HASH, 3>(P, stream, num_cus);
+    return launch_rs<4096, CS, HASH, 4>(P, stream, num_cus);
+  }
+  if (P.waves == 2) return launch_rs<8192, CS, HASH, 2>(P, stream, num_cus);
   if (P.options & kRegPrefix) return launch_rs<8192, CS, HASH, 3>(P, stream, num_cus);
   return launch_rs<8192, CS, HASH, 3, false, false>(P, stream, num_cus);
 }

@@ -323,7 +323,8 @@ typedef struct gpd_tuning {
                              -1 automatic (mean slot <= 96 B), 0 off, 1 on */
   int32_t  reg_prefix;    /* 8 KiB windows' chunk prefix sums from the registers at commit:
                              -1 automatic (mean slot > 160 B), 0 off, 1 on */
-  int32_t  reserved;
+  int32_t  waves_per_simd; /* resident waves of the fast kernel per SIMD: 0 automatic, 2, 3, 4
+                              (4 KiB windows) or 2, 3 (8 KiB windows) */
 } gpd_tuning;
 int  gpd_ctx_set_tuning(gpd_ctx *ctx, const gpd_tuning *t);
 const char *gpd_last_error_string(void);
