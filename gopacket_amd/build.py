@@ -40,9 +40,10 @@ def _stale(target, deps):
 
 def build_lib(force: bool = False, verbose: bool = False) -> str:
     if force or _stale(LIB, SOURCES + HEADERS):
+        extra = os.environ.get("GPD_EXTRA_CFLAGS", "").split()  # diagnostic builds (tools/)
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
                "-Wall", "-Wno-unused-function", "-pthread", "-I", os.path.join(ROOT, "include"),
-               *SOURCES, "-o", LIB + ".tmp"]
+               *extra, *SOURCES, "-o", LIB + ".tmp"]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
