@@ -775,6 +775,8 @@ def main():
     ap.add_argument("--shard-check", default="", help="tests only (CPU, gloo): build the replay "
                     "capture, cut and index this rank's shard, write its record positions to DIR")
     ap.add_argument("--chunk", type=int, default=0, help="tests only: records per index chunk")
+    ap.add_argument("--lean", action="store_true", help="only the timed launches (profiling runs: "
+                    "no 36-B record line, no fallback split, no CPU baseline)")
     args = ap.parse_args()
 
     env_world = os.environ.get("WORLD_SIZE")
@@ -913,7 +915,7 @@ def main():
     n_err = int(np.count_nonzero((st & 3) != 0))
     out = summarize(workload, n, world, args.steps, args.warmup, elapsed, kern_ms, kern_ms_max,
                     batch, n_err, interleaved=16 if pcap_info else 0)
-    if not args.ablate:  # the 36-B record (hdr_off on, as the flow table consumes it)
+    if not args.ablate and not args.lean:  # the 36-B record (hdr_off on, as the flow table uses)
         out["record36"] = bench_record36(parser, dev_batch, n, local, stream, out, args)
         out["fallback"] = bench_split(parser, dev_batch, dev_res, n, local, stream)
     if pcap_info:
@@ -932,7 +934,7 @@ def main():
     if args.ablate:
         out["ablation"] = args.ablate
         out["metric"] = "DIAGNOSTIC ablation (not the metric): " + out["metric"]
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.ablate:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.ablate and not args.lean:
         out["cpu_baseline"] = cpu_baseline(batch, args.cpu_budget / 3)
     if rank == 0:
         print(json.dumps(out), flush=True)

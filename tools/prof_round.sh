@@ -9,7 +9,7 @@ CFG=$1
 STEPS=${2:-20}
 D=gpurun_out/prof/$CFG
 mkdir -p "$D"
-B="python3 bench.py --config $CFG --steps $STEPS --warmup 3 --no-cpu-baseline"
+B="python3 bench.py --config $CFG --steps $STEPS --warmup 3 --lean ${EXTRA:-}"
 run() {  # name, rocprofv3 args...
   local name=$1; shift
   timeout -k 10 400 rocprofv3 "$@" --output-format csv -d "$D/$name" -o "$name" -- $B > "$D/$name.log" 2>&1

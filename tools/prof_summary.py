@@ -20,6 +20,21 @@ def kernel_stats(d):
     return out
 
 
+def per_stream(d):
+    """Decode-kernel launches grouped by HIP stream (config 5 runs its resident launches on one
+    stream and the host-streamed chunks on the staging slots' two)."""
+    out = {}
+    for f in glob.glob(os.path.join(d, "kt", "**", "*kernel_trace.csv"), recursive=True):
+        g = collections.defaultdict(list)
+        for r in csv.DictReader(open(f)):
+            if "rs_kernel" in r["Kernel_Name"] or "decode_kernel" in r["Kernel_Name"]:
+                g[r["Stream_Id"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+        for k, v in g.items():
+            out["stream_" + k] = {"calls": len(v), "avg_us": sum(v) / len(v), "min_us": min(v),
+                                  "max_us": max(v)}
+    return out
+
+
 def counters(d, name):
     acc = collections.defaultdict(list)
     meta = {}
@@ -34,7 +49,7 @@ def counters(d, name):
 
 
 def summarize(d):
-    s = {"kernels": kernel_stats(d)}
+    s = {"kernels": kernel_stats(d), "decode_kernel_by_stream": per_stream(d)}
     fetch, meta = counters(d, "fetch")
     write, _ = counters(d, "write")
     sq, _ = counters(d, "sq")
