@@ -108,11 +108,14 @@ struct Recs {  // one walked stretch of records
   std::vector<uint64_t> pos;  // record header positions
   std::vector<uint32_t> cap, wire;
   std::vector<uint64_t> ts;
+  bool lean = false;  // positions and capture lengths only (what a decode needs)
   void reserve(size_t n) {
     pos.reserve(n);
     cap.reserve(n);
-    wire.reserve(n);
-    ts.reserve(n);
+    if (!lean) {
+      wire.reserve(n);
+      ts.reserve(n);
+    }
   }
   size_t size() const { return pos.size(); }
   void clear() {  // keeps the capacity: a walk reused across calls touches no fresh pages
@@ -124,8 +127,10 @@ struct Recs {  // one walked stretch of records
   void push(uint64_t p, uint32_t c, uint32_t w, uint64_t t) {
     pos.push_back(p);
     cap.push_back(c);
-    wire.push_back(w);
-    ts.push_back(t);
+    if (!lean) {
+      wire.push_back(w);
+      ts.push_back(t);
+    }
   }
 };
 struct PcapSlice {
@@ -134,6 +139,7 @@ struct PcapSlice {
 struct PcapWalk {
   std::vector<Recs> R;          // per segment, then sequential re-walks
   size_t used = 0;              // stretches of R in use (the rest keep their allocations)
+  bool lean = false;            // record positions and capture lengths only (Recs::lean)
   std::vector<PcapSlice> plan;  // the walk, in order
   uint64_t n = 0, next_pos = 0;
   int stop = 0, threads = 0, met = 0, rewalks = 0;

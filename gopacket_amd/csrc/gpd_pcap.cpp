@@ -265,6 +265,7 @@ namespace {
 Recs &stretch(PcapWalk &W, size_t r) {
   if (W.R.size() <= r) W.R.resize(r + 1);
   W.R[r].clear();
+  W.R[r].lean = W.lean;
   return W.R[r];
 }
 
@@ -444,8 +445,8 @@ void pcap_emit(const PcapWalk &W, uint64_t base, uint32_t *off32, uint64_t *pos6
       for (size_t j = 0; j < sl.cnt; j++) off32[o + j] = (uint32_t)(r.pos[sl.j0 + j] + d);
     if (pos64) std::memcpy(pos64 + o, r.pos.data() + sl.j0, sl.cnt * 8);
     if (cap) std::memcpy(cap + o, r.cap.data() + sl.j0, sl.cnt * 4);
-    if (wire) std::memcpy(wire + o, r.wire.data() + sl.j0, sl.cnt * 4);
-    if (ts) std::memcpy(ts + o, r.ts.data() + sl.j0, sl.cnt * 8);
+    if (wire && !r.lean) std::memcpy(wire + o, r.wire.data() + sl.j0, sl.cnt * 4);
+    if (ts && !r.lean) std::memcpy(ts + o, r.ts.data() + sl.j0, sl.cnt * 8);
   };
   if (W.plan.size() <= 1) {
     if (!W.plan.empty()) one(0);

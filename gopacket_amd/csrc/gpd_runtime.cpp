@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -235,6 +236,7 @@ struct gpd_ctx {
     gpd_ext_rec *h_ext = nullptr, *d_ext = nullptr;
     uint64_t lo = 0, hi = 0;  // packet range in flight
     bool busy = false;
+    bool direct = false;      // its results go straight into the caller's (registered) arrays
   } slot[2];
   uint64_t slot_bytes = 0, slot_pkts = 0;
   // host ranges pinned with gpd_host_register (H2D reads them in place)
@@ -655,17 +657,48 @@ struct SlotGuard {
 
 static void drain_slot(gpd_ctx::Slot &s, const gpd_result *out) {
   const uint64_t m = s.hi - s.lo;
-  par_for(m, 1u << 16, [&](uint64_t a, uint64_t b) {
-    const uint64_t c = b - a;
-    std::memcpy(out->status + s.lo + a, s.h_status + a, c * 4);
-    std::memcpy(out->layers + s.lo + a, s.h_layers + a, c * 8);
-    if (out->csum) std::memcpy(out->csum + s.lo + a, s.h_csum + a, c * 4);
-    if (out->net_hash) std::memcpy(out->net_hash + s.lo + a, s.h_nh + a, c * 8);
-    if (out->tp_hash) std::memcpy(out->tp_hash + s.lo + a, s.h_th + a, c * 8);
-    if (out->hdr_off) std::memcpy(out->hdr_off + s.lo + a, s.h_hoff + a, c * 4);
-    if (out->ext) std::memcpy(out->ext + s.lo + a, s.h_ext + a, c * sizeof(gpd_ext_rec));
-  });
+  if (!s.direct) {
+    par_for(m, 1u << 16, [&](uint64_t a, uint64_t b) {
+      const uint64_t c = b - a;
+      std::memcpy(out->status + s.lo + a, s.h_status + a, c * 4);
+      std::memcpy(out->layers + s.lo + a, s.h_layers + a, c * 8);
+      if (out->csum) std::memcpy(out->csum + s.lo + a, s.h_csum + a, c * 4);
+      if (out->net_hash) std::memcpy(out->net_hash + s.lo + a, s.h_nh + a, c * 8);
+      if (out->tp_hash) std::memcpy(out->tp_hash + s.lo + a, s.h_th + a, c * 8);
+      if (out->hdr_off) std::memcpy(out->hdr_off + s.lo + a, s.h_hoff + a, c * 4);
+      if (out->ext) std::memcpy(out->ext + s.lo + a, s.h_ext + a, c * sizeof(gpd_ext_rec));
+    });
+  }
   s.busy = false;
+}
+
+// Results of packets [lo, lo + m) device -> host on the slot's stream: straight into the
+// caller's arrays when every one of them lies in registered memory (gpd_host_register; then
+// the drain copies nothing), else into the slot's pinned arrays for drain_slot to copy.
+static hipError_t results_d2h(gpd_ctx *ctx, gpd_ctx::Slot &s, const gpd_result *out, uint64_t lo,
+                              uint64_t m) {
+  auto reg = [&](const void *p, uint64_t bytes) {
+    return p == nullptr || ctx->is_registered(static_cast<const uint8_t *>(p), bytes);
+  };
+  s.direct = !out->ext && reg(out->status + lo, m * 4) && reg(out->layers + lo, m * 8) &&
+             reg(out->csum ? out->csum + lo : nullptr, m * 4) &&
+             reg(out->net_hash ? out->net_hash + lo : nullptr, m * 8) &&
+             reg(out->tp_hash ? out->tp_hash + lo : nullptr, m * 8) &&
+             reg(out->hdr_off ? out->hdr_off + lo : nullptr, m * 4);
+  auto cp = [&](void *host, const void *dev, uint64_t bytes) {
+    return hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, s.stream);
+  };
+  hipError_t e = cp(s.direct ? (void *)(out->status + lo) : (void *)s.h_status, s.d_status, m * 4);
+  if (e == hipSuccess) e = cp(s.direct ? (void *)(out->layers + lo) : (void *)s.h_layers, s.d_layers, m * 8);
+  if (e == hipSuccess && out->csum) e = cp(s.direct ? (void *)(out->csum + lo) : (void *)s.h_csum, s.d_csum, m * 4);
+  if (e == hipSuccess && out->net_hash)
+    e = cp(s.direct ? (void *)(out->net_hash + lo) : (void *)s.h_nh, s.d_nh, m * 8);
+  if (e == hipSuccess && out->tp_hash)
+    e = cp(s.direct ? (void *)(out->tp_hash + lo) : (void *)s.h_th, s.d_th, m * 8);
+  if (e == hipSuccess && out->hdr_off)
+    e = cp(s.direct ? (void *)(out->hdr_off + lo) : (void *)s.h_hoff, s.d_hoff, m * 4);
+  if (e == hipSuccess && out->ext) e = cp(s.h_ext, s.d_ext, m * sizeof(gpd_ext_rec));
+  return e;
 }
 
 int gpd_decode_host(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out) {
@@ -748,15 +781,7 @@ int gpd_decode_host(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out) {
                  out->hdr_off ? s.d_hoff : nullptr};
     rc = launch(ctx, &b, &r, s.stream, false);
     if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(s.h_status, s.d_status, m * 4, hipMemcpyDeviceToHost, s.stream));
-    HIP_TRY(hipMemcpyAsync(s.h_layers, s.d_layers, m * 8, hipMemcpyDeviceToHost, s.stream));
-    if (out->csum) HIP_TRY(hipMemcpyAsync(s.h_csum, s.d_csum, m * 4, hipMemcpyDeviceToHost, s.stream));
-    if (out->net_hash) HIP_TRY(hipMemcpyAsync(s.h_nh, s.d_nh, m * 8, hipMemcpyDeviceToHost, s.stream));
-    if (out->tp_hash) HIP_TRY(hipMemcpyAsync(s.h_th, s.d_th, m * 8, hipMemcpyDeviceToHost, s.stream));
-    if (out->hdr_off)
-      HIP_TRY(hipMemcpyAsync(s.h_hoff, s.d_hoff, m * 4, hipMemcpyDeviceToHost, s.stream));
-    if (out->ext)
-      HIP_TRY(hipMemcpyAsync(s.h_ext, s.d_ext, m * sizeof(gpd_ext_rec), hipMemcpyDeviceToHost, s.stream));
+    HIP_TRY(results_d2h(ctx, s, out, i, m));
     s.lo = i;
     s.hi = j;
     s.busy = true;
@@ -812,6 +837,13 @@ static void par_memcpy(uint8_t *dst, const uint8_t *src, uint64_t n, int nthread
   for (auto &t : th) t.join();
 }
 
+// Host-clock phases of this thread's last gpd_decode_pcap(_at) call (gpd_decode_pcap_last_times).
+static thread_local double g_pt_walk = 0, g_pt_walkwait = 0, g_pt_stage = 0, g_pt_sync = 0, g_pt_drain = 0,
+                           g_pt_total = 0;
+static double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 int gpd_decode_pcap(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, uint64_t max_n,
                     const gpd_result *out, uint64_t *n_out, uint64_t *next_pos, int *stop,
                     int nthreads) {
@@ -831,87 +863,158 @@ int gpd_decode_pcap_at(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, const gpd
   if (out->ext) return set_err(GPD_ERR_INVALID, "gpd_decode_pcap: ext records not supported");
   if (pos > len) return set_err(GPD_ERR_INVALID, "gpd_decode_pcap_at: pos beyond the buffer");
   if (nthreads <= 0) nthreads = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
-  int rc;
-  // The walk and its flattened positions are kept per thread across calls (a replay or
-  // capture loop calls again and again; fresh pages for 24 B per record cost more than the
-  // walk itself).
-  static thread_local gpd::PcapWalk W;
-  static thread_local std::vector<uint64_t> rp;
-  static thread_local std::vector<uint32_t> rcap;
-  const int wrc = gpd::pcap_walk(buf, len, *info, pos, max_n, nthreads, W);
-  std::string werr = wrc ? std::string(g_err) : std::string();
-  const uint64_t n = W.n;
-  if (rp.size() < n) {
-    rp.resize(n);
-    rcap.resize(n);
-  }
-  gpd::pcap_emit(W, 0, nullptr, rp.data(), rcap.data(), nullptr, nullptr);
-  *n_out = n;
-  if (next_pos) *next_pos = W.next_pos;
-  if (stop) *stop = W.stop;
+  *n_out = 0;
+  if (next_pos) *next_pos = pos;
+  if (stop) *stop = GPD_PCAP_STOP_LIMIT;
+  if (max_n == 0) return GPD_OK;
   HIP_TRY(hipSetDevice(ctx->device));
   const uint64_t kPkts = 1u << 20, kBytes = 256ull << 20;
-  rc = alloc_slots(ctx, kBytes, kPkts, false);
+  int rc = alloc_slots(ctx, kBytes, kPkts, false);
   if (rc) return rc;
   SlotGuard guard{ctx};
-  uint64_t i = 0;
+  // The record walk runs one part (kPkts records) ahead of the transfers, on a helper thread:
+  // while part q's chunks travel and decode, part q+1 is walked.  Two parts' walks and their
+  // flattened positions are kept per calling thread across calls (a replay or capture loop
+  // calls again and again; fresh pages for 24 B per record cost more than the walk itself).
+  struct Part {
+    gpd::PcapWalk W;
+    std::vector<uint64_t> rp;
+    std::vector<uint32_t> rcap;
+    int rc = 0;
+    std::string err;
+  };
+  static thread_local Part part[2];
+  const double t_call = now_ms();
+  g_pt_walk = g_pt_walkwait = g_pt_stage = g_pt_sync = g_pt_drain = 0;
+  double walk_ms = 0;  // (written by the walking thread, read after its join)
+  auto walk_part = [&](Part &P, uint64_t at, uint64_t m) {
+    const double t0 = now_ms();
+    P.W.lean = true;  // positions and capture lengths only
+    P.rc = gpd::pcap_walk(buf, len, *info, at, m, nthreads, P.W);
+    P.err = P.rc ? std::string(gpd_last_error_string()) : std::string();  // (the walker's thread)
+    if (P.rp.size() < P.W.n) {
+      P.rp.resize(P.W.n);
+      P.rcap.resize(P.W.n);
+    }
+    gpd::pcap_emit(P.W, 0, nullptr, P.rp.data(), P.rcap.data(), nullptr, nullptr);
+    walk_ms += now_ms() - t0;
+  };
+  uint64_t done = 0;  // records decoded (the output index of the next one)
+  int q = 0;
+  walk_part(part[0], pos, std::min(kPkts, max_n));
+  struct Joiner {  // every exit, errors included, waits for the walk running ahead
+    std::thread t;
+    ~Joiner() {
+      if (t.joinable()) t.join();
+    }
+  } ahead;
   int k = 0;
-  while (i < n) {
-    auto &s = ctx->slot[k];
-    if (s.busy) {
-      HIP_TRY(hipStreamSynchronize(s.stream));
-      drain_slot(s, out);
+  for (;;) {
+    Part &cur = part[q];
+    const uint64_t n = cur.W.n;
+    const bool more = cur.rc == GPD_OK && cur.W.stop == GPD_PCAP_STOP_LIMIT && n > 0 && done + n < max_n;
+    if (more)  // walk the next part while this one is staged
+      ahead.t = std::thread(walk_part, std::ref(part[q ^ 1]), cur.W.next_pos, std::min(kPkts, max_n - done - n));
+    uint64_t i = 0;
+    while (i < n) {
+      auto &s = ctx->slot[k];
+      if (s.busy) {
+        const double t0 = now_ms();
+        HIP_TRY(hipStreamSynchronize(s.stream));
+        const double t1 = now_ms();
+        drain_slot(s, out);
+        g_pt_sync += t1 - t0;
+        g_pt_drain += now_ms() - t1;
+      }
+      const double t_stage = now_ms();
+      // records [i, j) whose bytes (from the first one's data, rounded down to 16) fit the slot
+      const uint64_t base = (cur.rp[i] + GPD_PCAP_RECORD_BYTES) & ~15ull;
+      uint64_t j = i;
+      while (j < n && j - i < kPkts && cur.rp[j] + GPD_PCAP_RECORD_BYTES + cur.rcap[j] - base <= kBytes) j++;
+      if (j == i) {
+        return set_err(GPD_ERR_INVALID, "gpd_decode_pcap: record %llu larger than %llu bytes",
+                       (unsigned long long)(done + i), (unsigned long long)kBytes);
+      }
+      const uint64_t m = j - i;
+      const uint64_t end = cur.rp[j - 1] + GPD_PCAP_RECORD_BYTES + cur.rcap[j - 1];
+      const uint64_t span = end - base;
+      // (plain pointers: the worker threads would see their own thread_local vectors)
+      const uint64_t *RP = cur.rp.data() + i;
+      const uint32_t *RC = cur.rcap.data() + i;
+      par_for(m, 1u << 16, [&](uint64_t a, uint64_t b) {
+        for (uint64_t p = a; p < b; p++) s.h_off[p] = (uint32_t)(RP[p] + GPD_PCAP_RECORD_BYTES - base);
+        std::memcpy(s.h_len + a, RC + a, (b - a) * 4);
+      });
+      const uint8_t *src = buf + base;
+      if (!ctx->is_registered(src, span)) {  // (a shard registers only its own bytes)
+        par_memcpy(s.h_data, src, span, nthreads);
+        src = s.h_data;
+      }
+      hipError_t e = hipMemcpyAsync(s.d_data, src, span, hipMemcpyHostToDevice, s.stream);
+      if (e == hipSuccess) e = hipMemcpyAsync(s.d_off, s.h_off, m * 4, hipMemcpyHostToDevice, s.stream);
+      if (e == hipSuccess) e = hipMemcpyAsync(s.d_len, s.h_len, m * 4, hipMemcpyHostToDevice, s.stream);
+      if (e != hipSuccess) {
+        return set_err(GPD_ERR_HIP, "gpd_decode_pcap: H2D: %s", hipGetErrorString(e));
+      }
+      gpd_batch b{s.d_data, span, s.d_off, s.d_len, m};
+      gpd_result r{s.d_status, s.d_layers, s.d_nh, s.d_th, s.d_csum, nullptr,
+                   out->hdr_off ? s.d_hoff : nullptr};
+      rc = launch(ctx, &b, &r, s.stream, false);
+      if (rc) return rc;
+      e = results_d2h(ctx, s, out, done + i, m);
+      if (e != hipSuccess) {
+        return set_err(GPD_ERR_HIP, "gpd_decode_pcap: D2H: %s", hipGetErrorString(e));
+      }
+      g_pt_stage += now_ms() - t_stage;
+      s.lo = done + i;
+      s.hi = done + j;
+      s.busy = true;
+      i = j;
+      k ^= 1;
     }
-    // records [i, j) whose bytes (from the first one's data, rounded down to 16) fit the slot
-    const uint64_t base = (rp[i] + GPD_PCAP_RECORD_BYTES) & ~15ull;
-    uint64_t j = i;
-    while (j < n && j - i < kPkts && rp[j] + GPD_PCAP_RECORD_BYTES + rcap[j] - base <= kBytes) j++;
-    if (j == i) return set_err(GPD_ERR_INVALID, "gpd_decode_pcap: record %llu larger than %llu bytes",
-                               (unsigned long long)i, (unsigned long long)kBytes);
-    const uint64_t m = j - i;
-    const uint64_t end = rp[j - 1] + GPD_PCAP_RECORD_BYTES + rcap[j - 1];
-    const uint64_t span = end - base;
-    // (plain pointers: the worker threads would see their own thread_local vectors)
-    const uint64_t *RP = rp.data() + i;
-    const uint32_t *RC = rcap.data() + i;
-    par_for(m, 1u << 16, [&](uint64_t a, uint64_t b) {
-      for (uint64_t p = a; p < b; p++) s.h_off[p] = (uint32_t)(RP[p] + GPD_PCAP_RECORD_BYTES - base);
-      std::memcpy(s.h_len + a, RC + a, (b - a) * 4);
-    });
-    const uint8_t *src = buf + base;
-    if (!ctx->is_registered(src, span)) {  // (a shard registers only its own bytes)
-      par_memcpy(s.h_data, src, span, nthreads);
-      src = s.h_data;
+    done += n;
+    *n_out = done;
+    if (next_pos) *next_pos = cur.W.next_pos;
+    if (stop) *stop = cur.W.stop;
+    if (!more) {
+      if (cur.rc) {  // the walk stopped at a record the reference rejects: decode what preceded it
+        for (auto &s : ctx->slot)
+          if (s.busy) {
+            HIP_TRY(hipStreamSynchronize(s.stream));
+            drain_slot(s, out);
+          }
+        return set_err(cur.rc, "%s", cur.err.c_str());
+      }
+      break;
     }
-    HIP_TRY(hipMemcpyAsync(s.d_data, src, span, hipMemcpyHostToDevice, s.stream));
-    HIP_TRY(hipMemcpyAsync(s.d_off, s.h_off, m * 4, hipMemcpyHostToDevice, s.stream));
-    HIP_TRY(hipMemcpyAsync(s.d_len, s.h_len, m * 4, hipMemcpyHostToDevice, s.stream));
-    gpd_batch b{s.d_data, span, s.d_off, s.d_len, m};
-    gpd_result r{s.d_status, s.d_layers, s.d_nh, s.d_th, s.d_csum, nullptr,
-                 out->hdr_off ? s.d_hoff : nullptr};
-    rc = launch(ctx, &b, &r, s.stream, false);
-    if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(s.h_status, s.d_status, m * 4, hipMemcpyDeviceToHost, s.stream));
-    HIP_TRY(hipMemcpyAsync(s.h_layers, s.d_layers, m * 8, hipMemcpyDeviceToHost, s.stream));
-    if (out->csum) HIP_TRY(hipMemcpyAsync(s.h_csum, s.d_csum, m * 4, hipMemcpyDeviceToHost, s.stream));
-    if (out->net_hash) HIP_TRY(hipMemcpyAsync(s.h_nh, s.d_nh, m * 8, hipMemcpyDeviceToHost, s.stream));
-    if (out->tp_hash) HIP_TRY(hipMemcpyAsync(s.h_th, s.d_th, m * 8, hipMemcpyDeviceToHost, s.stream));
-    if (out->hdr_off)
-      HIP_TRY(hipMemcpyAsync(s.h_hoff, s.d_hoff, m * 4, hipMemcpyDeviceToHost, s.stream));
-    s.lo = i;
-    s.hi = j;
-    s.busy = true;
-    i = j;
-    k ^= 1;
+    const double tj = now_ms();
+    ahead.t.join();
+    g_pt_walkwait += now_ms() - tj;
+    q ^= 1;
   }
   for (auto &s : ctx->slot) {
     if (s.busy) {
+      const double t0 = now_ms();
       HIP_TRY(hipStreamSynchronize(s.stream));
+      const double t1 = now_ms();
       drain_slot(s, out);
+      g_pt_sync += t1 - t0;
+      g_pt_drain += now_ms() - t1;
     }
   }
-  if (wrc) return set_err(wrc, "%s", werr.c_str());
+  g_pt_walk = walk_ms;
+  g_pt_total = now_ms() - t_call;
   return GPD_OK;
+}
+
+void gpd_decode_pcap_last_times(double *ms6) {
+  if (!ms6) return;
+  ms6[0] = g_pt_total;     // the whole call
+  ms6[1] = g_pt_walk;      // record walks (the first on the caller, the rest ahead on a helper)
+  ms6[2] = g_pt_walkwait;  // waiting for a walk running ahead
+  ms6[3] = g_pt_stage;     // descriptor rebase, staging copies, issuing transfers and launches
+  ms6[4] = g_pt_sync;      // waiting for a slot's transfers and decode
+  ms6[5] = g_pt_drain;     // copying a slot's results out (none with registered result arrays)
 }
 
 }  // extern "C"

@@ -124,6 +124,11 @@ int gpd_pcap_locate(const uint8_t *buf, uint64_t len, const gpd_pcap_info *info,
                     const uint64_t *targets, uint64_t k, uint64_t *pos_out, uint64_t *n_total, int *stop,
                     int nthreads);
 
+/* Diagnostics: host-clock phases (ms) of this thread's last gpd_decode_pcap(_at) call: total,
+ * record walks, waiting for a walk running ahead, staging and issuing, waiting for slots,
+ * copying results out. */
+void gpd_decode_pcap_last_times(double *ms6);
+
 /* Diagnostics of this thread's last walk: segments walked in parallel, segments whose
  * speculation the true walk met, segments re-walked sequentially. */
 void gpd_pcap_last_stats(int *threads, int *met, int *rewalks);

@@ -406,3 +406,40 @@ def test_host_path_recovers_after_a_failed_call():
     nxt = synth.make_mixed(5000, seed=0x77)
     ref = O.decode(nxt, L.LayerTypeEthernet, ALL, 0, ext=False, nthreads=8)
     assert_same(p.DecodeBatchHost(nxt), ref, nxt, ext=False)
+
+
+def test_host_paths_into_registered_result_arrays():
+    """Result arrays registered with gpd_host_register receive the results by DMA (no staging
+    copy): gpd_decode_host and gpd_decode_pcap_at must give the same words either way."""
+    from gopacket_amd import parser as P
+    from gopacket_amd import pcap as NP
+    from gopacket_amd._lib import check, lib
+    from gopacket_amd.results import BatchResult
+    b = synth.make_mixed(9000)
+    p = P.DecodingLayerParser(L.LayerTypeEthernet)
+    p._mask = ALL
+    ref = p.DecodeBatchHost(b)
+    z = lambda dt: np.zeros(b.n, dt)
+    out = BatchResult(z(np.uint32), z(np.uint64), z(np.uint64), z(np.uint64), z(np.uint32), None,
+                      z(np.uint32))
+    arrs = [out.status, out.layers, out.net_hash, out.tp_hash, out.csum, out.hdr_off]
+    h = p.ctx().h
+    for a in arrs:
+        check(lib.gpd_host_register(h, a.ctypes.data, a.nbytes), "register")
+    try:
+        assert_same(p.DecodeBatchHost(b, out=out), ref, b, ext=False)
+        cap = NP.synth_capture(synth.make_udp64(3 << 18))  # 3 parts of 2^18 records
+        info = NP.header(cap)
+        want = p.DecodeBatch(NP.index(cap).batch)
+        m = 3 << 18
+        big = BatchResult(np.zeros(m, np.uint32), np.zeros(m, np.uint64), np.zeros(m, np.uint64),
+                          np.zeros(m, np.uint64), np.zeros(m, np.uint32), None, np.zeros(m, np.uint32))
+        for a in (big.status, big.layers, big.net_hash, big.tp_hash, big.csum, big.hdr_off):
+            check(lib.gpd_host_register(h, a.ctypes.data, a.nbytes), "register")
+            arrs.append(a)
+        k, nxt, stop, err = p.DecodePcapAt(cap, info, 24, m, big)
+        assert k == m and err is None and stop == NP.STOP_LIMIT
+        assert_same(big, want, None, ext=False)
+    finally:
+        for a in arrs:
+            lib.gpd_host_unregister(h, a.ctypes.data)
