@@ -45,8 +45,8 @@ CONFIGS = {
     "vxlan": ("config4: 2^23 x 128 B Eth/IPv4/UDP/VXLAN/Eth/IPv4/TCP, inner flow keys, "
               "synthetic seed 0x5EED0004", 1 << 23),
     "mixed": ("traffic mix (not a BASELINE config): 2^22 frames of TCP 64/576/1500, UDP 64, VXLAN, "
-              "ICMPv4 echo, IPv6/TCP, 802.3/LLC (fast kernel) and IPv4 options, fragments, IPv6 "
-              "hop-by-hop, cut TCP headers (12 %, generic decoder); every decoder registered, "
+              "ICMPv4 echo, IPv6/TCP (fast kernel) and 802.3/LLC/STP, IPv4 options, fragments, "
+              "IPv6 hop-by-hop, cut TCP headers (12 %, generic decoder); every decoder registered, "
               "synthetic seed 0x5EED0007", 1 << 22),
     "pcap64": ("config5 (per GPU): a pcap capture of 2^24 x 64 B Eth/IPv4/UDP records decoded in "
                "place (the capture bytes are the batch buffer: 16-B record headers interleaved), "

@@ -383,7 +383,7 @@ def _mix_class(name: str, m: int, seed: int, free_t, free_u) -> np.ndarray:
 def make_traffic_mix(n: int, seed: int = 0x5EED0007, align: int = 16) -> PacketBatch:
     """A seeded mix of MIX_CLASSES by weight, shuffled: TCP 64/576/1500, UDP 64, VXLAN, ICMPv4
     echo and IPv6/TCP frames that the fast kernel decodes, plus 802.3/LLC frames, IPv4 options,
-    IPv4 fragments, IPv6 hop-by-hop and cut TCP headers (13 %, MIX_FALLBACK) that it leaves to
+    IPv4 fragments, IPv6 hop-by-hop and cut TCP headers (12 %, MIX_FALLBACK) that it leaves to
     the generic decoder.  Checksums are valid except 1 in 64 TCP frames."""
     wsum = sum(w for _, _, w in MIX_CLASSES)
     counts = [n * w // wsum for _, _, w in MIX_CLASSES]
