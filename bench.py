@@ -533,9 +533,11 @@ def bench_replay(args, world, rank, local, dist):
     cpos, cn, _ = NP.locate(cap, [a for a, _ in chunks] + [m], pos=start, data_len=end, nthreads=threads)
     assert cn == m and int(cpos[-1]) == end
     t_locate = time.perf_counter() - t0
-    parser = P.NewDecodingLayerParser(L.LayerTypeEthernet, P.Ethernet(), P.Dot1Q(), P.IPv4(),
-                                      P.IPv6(), P.IPv6ExtensionSkipper(), P.TCP(), P.UDP(),
-                                      P.VXLAN(), P.Payload(), P.Fragment(), device=local)
+    layers = [P.Ethernet(), P.Dot1Q(), P.IPv4(), P.IPv6(), P.IPv6ExtensionSkipper(), P.TCP(),
+              P.UDP(), P.VXLAN(), P.Payload(), P.Fragment()]
+    if args.decoders == "novxlan":
+        layers = [d for d in layers if not isinstance(d, P.VXLAN)]
+    parser = P.NewDecodingLayerParser(L.LayerTypeEthernet, *layers, device=local)
     h = parser.ctx().h
     # pin the shard's pages (the H2D of both legs reads them in place)
     reg_lo, reg_hi = start & ~4095, min(len(cap), (end + 4095) & ~4095)
@@ -775,6 +777,8 @@ def main():
     ap.add_argument("--tpv3", action="store_true",
                     help="diagnostic: walk + decode a TPACKET_V3 ring of the config's packets "
                     "(gpd_decode_tpv3, PCIe-inclusive); printed as a separate line")
+    ap.add_argument("--decoders", default="all", choices=("all", "novxlan"),
+                    help="registered decoders: all of the engine's set, or without VXLAN")
     ap.add_argument("--ablate", default="", help="diagnostics only: 'nocsum', 'nohash' or both "
                     "(comma separated); never used for the reported metric")
     ap.add_argument("--tune", default="", help="A/B only: engine tuning, e.g. 'shift=0' or "
@@ -840,9 +844,11 @@ def main():
                      "index_threads": NP.last_walk_stats()[0]}
     dev_batch = P.DeviceBatch(batch, local)
     dev_res = P.DeviceResult(n, local, ext=False, hdr_off=False)  # the 32-B record
-    parser = P.NewDecodingLayerParser(L.LayerTypeEthernet, P.Ethernet(), P.Dot1Q(), P.IPv4(),
-                                      P.IPv6(), P.IPv6ExtensionSkipper(), P.TCP(), P.UDP(),
-                                      P.VXLAN(), P.Payload(), P.Fragment(), device=local)
+    layers = [P.Ethernet(), P.Dot1Q(), P.IPv4(), P.IPv6(), P.IPv6ExtensionSkipper(), P.TCP(),
+              P.UDP(), P.VXLAN(), P.Payload(), P.Fragment()]
+    if args.decoders == "novxlan":
+        layers = [d for d in layers if not isinstance(d, P.VXLAN)]
+    parser = P.NewDecodingLayerParser(L.LayerTypeEthernet, *layers, device=local)
     if args.config == "mixed":  # the reference benchmark's set and more: ICMPv4 and LLC too
         parser.AddDecodingLayer(P.ICMPv4())
         parser.AddDecodingLayer(P.LLC())

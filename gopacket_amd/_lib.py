@@ -11,7 +11,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libgpd.so")
 
-GPD_ABI_VERSION = 4
+GPD_ABI_VERSION = 5
 GPD_OK = 0
 
 
@@ -34,7 +34,7 @@ class GpdResult(C.Structure):
 
 class GpdTuning(C.Structure):
     _fields_ = [("window_bytes", C.c_uint32), ("shift", C.c_int32), ("reg_prefix", C.c_int32),
-                ("waves_per_simd", C.c_int32)]
+                ("waves_per_simd", C.c_int32), ("header_once", C.c_int32)]
 
 
 class GpdPcapInfo(C.Structure):

@@ -47,8 +47,9 @@ constexpr uint32_t kDiagNtLoad = 1u << 29;      // A/B: window LDS-DMA with the 
 constexpr uint32_t kDiagNtStore = 1u << 28;     // A/B: result stores with the nt cache policy
 constexpr uint32_t kShiftWindows = 1u << 27;    // internal: register-staged windows copied shifted
 constexpr uint32_t kRegPrefix = 1u << 26;       // internal: 8 KiB windows of long frames (IMIX)
+constexpr uint32_t kHeaderOnce = 1u << 25;      // internal: 8 KiB windows decoded once per tile (seg_pass)
 constexpr uint32_t kDiagMask = kDiagSkipDecode | kDiagNoWait | kDiagNtLoad | kDiagNtStore | kShiftWindows |
-                               kRegPrefix;
+                               kRegPrefix | kHeaderOnce;
 
 extern __shared__ __attribute__((aligned(16))) uint8_t g_lds[];
 
@@ -790,6 +791,153 @@ __device__ __forceinline__ void window_prefix(uint32_t buf, uint32_t pfx, uint32
   if (lane == 63u) *reinterpret_cast<uint32_t *>(g_lds + pfx + 4u * K * 64u) = incl;
 }
 
+// Header-once decode (rs_kernel HO, windows of long frames): a tile of 64 such packets spans
+// several windows, and a straight-line decode per window would run with the few lanes whose
+// packets that window holds.  Instead, in the window that holds a packet, seg_pass keeps
+// the bytes the decode reads in the lane's registers and sums the transport segment the
+// decode will checksum; after the tile's last window fast_decode<HO> runs once for all 64
+// lanes from those registers.
+struct Hdr {
+  uint32_t e1, e2, e3;  // frame bytes 12..23: EtherType and up to two tags (ld128(p + 8).y/z/w)
+  uint32_t W[16];       // the 64 bytes from the network header on
+  uint32_t pos;         // tp_off | tp_len << 16 of the segment summed (0xFFFFFFFF: none)
+  uint32_t sum;         // its LE-domain byte sum, pseudo-header not included
+  uint32_t ok;          // its TCP options parse (tcp.go:274-300); 2: a VXLAN payload follows
+};
+
+// The LE-domain sum s + bytes [S, S + len) of the window, read as its first 16-byte chunk, the
+// whole chunks after it and the ragged tail (TCP.ComputeChecksum's loop, tcpip.go:52-88).
+__device__ __forceinline__ uint32_t seg_sum_chunks(uint32_t S, uint32_t len, uint32_t s) {
+  const U128 c0 = ld128(S), ct = ld128(S + (len & ~15u));
+  const uint32_t w0 = len >= 16u ? 0x00010001u : 0u;  // first whole chunk
+  s = dot2(c0.x, w0, s);
+  s = dot2(c0.y, w0, s);
+  s = dot2(c0.z, w0, s);
+  s = dot2(c0.w, w0, s);
+  const uint32_t r8 = (len & 15u) * 8u;  // ragged tail: an odd last byte is its half's low byte
+  uint64_t lo = ((uint64_t)ct.y << 32) | ct.x, hi = ((uint64_t)ct.w << 32) | ct.z;
+  lo = r8 >= 64u ? lo : (r8 ? (lo << (64u - r8)) >> (64u - r8) : 0ull);
+  hi = r8 > 64u ? (hi << (128u - r8)) >> (128u - r8) : 0ull;
+  s = dot2((uint32_t)lo, 0x00010001u, s);
+  s = dot2((uint32_t)(lo >> 32), 0x00010001u, s);
+  s = dot2((uint32_t)hi, 0x00010001u, s);
+  s = dot2((uint32_t)(hi >> 32), 0x00010001u, s);
+  const uint32_t xt = len & ~15u;
+  for (uint32_t x = 16; x < xt; x += 16u) {
+    const U128 q = ld128(S + x);
+    s = dot2(q.x, 0x00010001u, s);
+    s = dot2(q.y, 0x00010001u, s);
+    s = dot2(q.z, 0x00010001u, s);
+    s = dot2(q.w, 0x00010001u, s);
+  }
+  return s;
+}
+
+// seg_pass: the first round trip of fast_decode (the Ethernet and network header bytes) kept
+// in h, and the segment that fast_decode's guesses lead to (IPv4 IHL 5 / IPv6 by the version
+// nibble, TCP / UDP by the protocol number, UDP Length) summed from this window: its head
+// and tail here, the whole chunks between left to the window's chunk prefix sums (sg) when it
+// is long and even-aligned.  fast_decode<HO> confirms the guesses with the dispatch tables and
+// uses the sum only when its own transport segment is exactly h.pos (else the packet takes
+// the generic decoder).  With VXLAN registered (vxreg), a UDP segment whose ports lead to it
+// is flagged (h.ok = 2) for the full decode in this window: its inner headers are not staged.
+template <bool COOP>
+__device__ __forceinline__ void seg_pass(uint32_t p, uint32_t len, uint32_t buf, Hdr &h, Seg &sg,
+                                         const FastCtx &F, bool vxreg) {
+  h.pos = 0xFFFFFFFFu;
+  h.sum = 0;
+  h.ok = 0;
+  if (len < 15u) return;
+  const U128 e = ld128(p + 8);
+  load64(h.W, p + 14);
+  h.e1 = e.y;
+  h.e2 = e.z;
+  h.e3 = e.w;
+  const uint32_t et0 = be_lo(e.y), et1 = be_lo(e.z);
+  if (et0 < 0x0600u) return;
+  const uint32_t t1 = tag_type(et0), t2 = t1 & tag_type(et1);
+  const uint32_t l3 = 14 + 4 * (t1 + t2);
+  if (t1) load64(h.W, p + l3);
+  if (len < l3 + 20u) return;
+  const uint32_t *W = h.W;
+  const uint32_t ver = (W[0] >> 4) & 15u;
+  const bool v4 = ver == 4u;
+  const uint32_t dl = len - l3;
+  const uint32_t length = v4 ? be_hi(W[0]) : be_lo(W[1]);
+  uint32_t plen;
+  if (v4) {
+    if ((W[0] & 0x0Fu) != 5u || length < 20u) return;
+    plen = (dl > length ? length : dl) - 20u;
+  } else {
+    if (ver != 6u || dl < 40u) return;
+    plen = (length > dl - 40u) ? dl - 40u : length;
+  }
+  const uint32_t proto = v4 ? ((W[2] >> 8) & 0xFFu) : ((W[1] >> 16) & 0xFFu);
+  const uint32_t g = proto == 6u ? 1u : (proto == 17u ? 2u : 0u);
+  if (!g) return;
+  const uint32_t ty = v4 ? W[6] : W[11], tw = v4 ? W[8] : W[13];
+  const uint32_t l4 = l3 + (v4 ? 20u : 40u);
+  const uint32_t ulen = be_lo(ty);
+  const uint32_t seg = (g == 2u && ulen >= 8u && ulen <= plen) ? ulen : plen;
+  if (vxreg && g == 2u) {  // ports -> VXLAN (udp.go:108-110 NextLayerType by port)
+    const uint32_t tx = v4 ? W[5] : W[10];
+    const uint32_t rd = fix_bucket_at(kFixUdpBase, F.mult, be_hi(tx));
+    const uint32_t rs = fix_bucket_at(kFixUdpBase, F.mult, be_lo(tx));
+    if ((ports_next_raw(rd, rs, F.pl_raw) & 15u) == D_VXLAN) {
+      h.ok = 2;
+      return;
+    }
+  }
+  if (g == 1u) {  // the options walk of fast_decode, on the guess
+    const uint32_t hl = ((tw >> 4) & 15u) * 4u;
+    uint32_t ok = (plen >= 20u && hl >= 20u && hl <= plen) ? 1u : 0u;
+    for (uint32_t q = 20; ok && q < hl;) {
+      const uint32_t k = g_lds[p + l4 + q];
+      if (k == 0) break;
+      uint32_t ol = 1;
+      if (k != 1) {
+        if (hl - q < 2) { ok = 0; break; }
+        ol = g_lds[p + l4 + q + 1];
+        if (ol < 2 || ol > hl - q) { ok = 0; break; }
+      }
+      q += ol;
+    }
+    h.ok = ok;
+  }
+  h.pos = l4 | (seg << 16);
+  const uint32_t S = p + l4;
+  if (COOP && seg >= 64u && !(S & 1u)) {
+    // head [S, A) and tail [B, E) from their aligned chunks; [A, B) from the prefix sums
+    const uint32_t E = S + seg, A = (S + 15u) & ~15u, B = E & ~15u;
+    uint32_t s = 0;
+    if (A > S) {
+      const uint4 q = *reinterpret_cast<const uint4 *>(g_lds + A - 16u);
+      const uint32_t h8 = (S & 15u) * 8u;
+      uint64_t lo = ((uint64_t)q.y << 32) | q.x, hi = ((uint64_t)q.w << 32) | q.z;
+      lo = h8 >= 64u ? 0ull : (lo >> h8) << h8;
+      hi = h8 > 64u ? (hi >> (h8 - 64u)) << (h8 - 64u) : hi;
+      s = dot2((uint32_t)lo, 0x00010001u, s);
+      s = dot2((uint32_t)(lo >> 32), 0x00010001u, s);
+      s = dot2((uint32_t)hi, 0x00010001u, s);
+      s = dot2((uint32_t)(hi >> 32), 0x00010001u, s);
+    }
+    if (E > B) {
+      const uint4 q = *reinterpret_cast<const uint4 *>(g_lds + B);
+      const uint32_t r8 = (E & 15u) * 8u;
+      uint64_t lo = ((uint64_t)q.y << 32) | q.x, hi = ((uint64_t)q.w << 32) | q.z;
+      lo = r8 >= 64u ? lo : (lo << (64u - r8)) >> (64u - r8);
+      hi = r8 > 64u ? (hi << (128u - r8)) >> (128u - r8) : 0ull;
+      s = dot2((uint32_t)lo, 0x00010001u, s);
+      s = dot2((uint32_t)(lo >> 32), 0x00010001u, s);
+      s = dot2((uint32_t)hi, 0x00010001u, s);
+      s = dot2((uint32_t)(hi >> 32), 0x00010001u, s);
+    }
+    sg = Seg{s, (A - buf) >> 4, (B - buf) >> 4};  // the caller adds P[b] - P[a] into h.sum
+    return;
+  }
+  h.sum = seg_sum_chunks(S, seg, 0u);
+}
+
 // p: LDS address of the packet's first byte; len: its length.  CS / HASH: the fused
 // checksums / flow hashes are requested (GPD_OPT_NO_CHECKSUMS / _NO_FLOW_HASH clear).
 // Two dependent LDS round trips per pass (three for tagged frames): (1) the Ethernet header
@@ -801,9 +949,11 @@ __device__ __forceinline__ void window_prefix(uint32_t buf, uint32_t pfx, uint32
 // layer objects are overwritten (A11); the transport checksum reads its segment's edge
 // chunks once more after the parse.
 // COOP: a long even-aligned segment's whole middle chunks are left to window_prefix (sg).
-template <bool CS, bool HASH, bool COOP>
+// HO: the header-once decode — no window is read: the header bytes and the segment sum come
+// from seg_pass (*h), one pass (a VXLAN payload takes the generic decoder).
+template <bool CS, bool HASH, bool COOP, bool HO = false>
 __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const FastCtx &F, Out &o,
-                                            uint32_t buf, Seg &sg) {
+                                            uint32_t buf, Seg &sg, const Hdr *h = nullptr) {
   uint64_t codes = 0, nh = 0, th = 0;
   uint32_t nc = 0, trunc = 0, stop = 0;
   uint32_t net = 0, tp = 0, ip4 = 0, ipcs = 0;
@@ -812,17 +962,27 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
   uint32_t net_off = 0;                        // the last network header
   uint32_t b = 0, lim = len;                   // this pass's Ethernet offset; end of its data
   auto put = [&](uint32_t code) { codes |= (uint64_t)code << (16 + 4 * nc); nc++; };
-  for (int pass = 0; pass < 2; pass++) {
+  for (int pass = 0; pass < (HO ? 1 : 2); pass++) {
     // ---- round trip 1: Ethernet header (ethernet.go:41-62) and the bytes after it
     if (lim < b + 15u) return false;  // too small, or an empty payload: generic path
-    const U128 e = ld128(p + b + 8);  // bytes 8..23: EtherType and up to two tags
+    U128 e;  // bytes 8..23: EtherType and up to two tags
     uint32_t W[16];
-    load64(W, p + b + 14);
+    if (HO) {
+      e.x = 0;
+      e.y = h->e1;
+      e.z = h->e2;
+      e.w = h->e3;
+#pragma unroll
+      for (int k = 0; k < 16; k++) W[k] = h->W[k];
+    } else {
+      e = ld128(p + b + 8);
+      load64(W, p + b + 14);
+    }
     const uint32_t et0 = be_lo(e.y), et1 = be_lo(e.z), et2 = be_lo(e.w);
     if (et0 < 0x0600u) return false;  // 802.3 length framing (LLC): the generic decoder
     const uint32_t t1 = tag_type(et0), t2 = t1 & tag_type(et1);
     const uint32_t l3 = b + 14 + 4 * (t1 + t2);
-    if (t1) load64(W, p + l3);  // tagged: the network header is further in
+    if (t1 && !HO) load64(W, p + l3);  // tagged: the network header is further in
     // ---- guesses from the bytes
     const uint32_t ver = (W[0] >> 4) & 15u;
     const bool v4 = ver == 4u;
@@ -920,7 +1080,8 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
     if (g == 1u) {  // tcp.go:229-314
       hl = ((tw >> 4) & 15u) * 4u;
       if (plen < 20u || hl < 20u || hl > plen) return false;
-      for (uint32_t q = 20; q < hl;) {  // OPTIONS, tcp.go:274-300 (errors -> generic path)
+      if (HO && !h->ok) return false;
+      for (uint32_t q = 20; !HO && q < hl;) {  // OPTIONS, tcp.go:274-300 (errors -> generic path)
         const uint32_t k = g_lds[p + l4 + q];
         if (k == 0) break;
         uint32_t ol = 1;
@@ -954,7 +1115,7 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
     const uint32_t next = ports_next_raw(rd, rs, F.pl_raw), nd = next & 15u;
     if (nd == D_NONE) { stop = (next >> 8) & 0xFFu; break; }
     if (nd == D_PAYLOAD) { put(GPD_C_PAYLOAD); break; }  // Payload consumes the rest
-    if (nd != D_VXLAN || pass == 1 || pl4 < 8u) return false;
+    if (HO || nd != D_VXLAN || pass == 1 || pl4 < 8u) return false;
     put(GPD_C_VXLAN);  // vxlan.go:53-78; its payload is an Ethernet frame (A11: two passes)
     b = l4 + hl + 8;
     if (pl4 == 8u) break;
@@ -966,7 +1127,13 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
   st |= (net << 20) | (tp ? (tp == 1 ? 4u : 5u) << 24 : 0u);  // endpoint types (gpd.h)
   if (HASH) st |= (net ? 1u << 16 : 0u) | (tp ? 1u << 17 : 0u);
   sg.b = 0;
-  if (COOP && CS && tp && tp_len >= 64u && !((p + tp_off) & 1u)) {
+  if (HO) {
+    if (CS) {  // the segment seg_pass summed must be this transport's
+      if (tp && h->pos != (tp_off | (tp_len << 16))) return false;
+      cs = (ip4 ? ipcs : 0u) | (tp ? fold_le_not(tp_ps + h->sum) << 16 : 0u);
+      st |= (ip4 ? 1u << 18 : 0u) | (tp ? 1u << 19 : 0u);
+    }
+  } else if (COOP && CS && tp && tp_len >= 64u && !((p + tp_off) & 1u)) {
     // head [S, A) and tail [B, E) from their aligned chunks; [A, B) from the prefix sums
     const uint32_t S = p + tp_off, E = S + tp_len, A = (S + 15u) & ~15u, B = E & ~15u;
     uint32_t s = tp_ps;
@@ -1000,8 +1167,7 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
     o.csum = ip4 ? ipcs : 0u;  // the transport half is added by the caller
     o.hoff = hdr_word(net != 0, net_off, tp != 0, tp_off);
     return true;
-  }
-  if (CS) {
+  } else if (CS) {
     // TCP.ComputeChecksum(), tcp.go:193-195 / tcpip.go:52-88 over the last transport.  Its
     // first and ragged-last 16-byte chunks are read here, once, after the parse (holding
     // them through the parse would cost 16 VGPRs, a wave per SIMD).
@@ -1463,7 +1629,7 @@ __device__ __forceinline__ void rows_prefix(const uint32_t (&cs)[NC], uint32_t p
 // window finished (deferred one iteration, so that after the next window's loads nothing else
 // is issued and the wait at the next commit covers exactly those loads)  ->  plan and load
 // window k+1  ->  decode window k from LDS.
-template <int STAGE, bool CS, bool HASH, int MINW, bool DEFER = false, bool RPFX = true>
+template <int STAGE, bool CS, bool HASH, int MINW, bool DEFER = false, bool RPFX = true, bool HO = false>
 __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
   constexpr int WAVES = 4;
   constexpr int NC = STAGE / 1024;              // 16-byte chunks per lane per window
@@ -1580,6 +1746,9 @@ __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
   bool first_d = true;
   Out res{0, 0, 0, 0, 0, 0};
   uint32_t fb = 0;
+  Hdr hh{};          // HO: the lane's packet as seg_pass staged it
+  uint32_t got = 0;  // HO: ... in one of this tile's windows (2: decoded there in full)
+  const bool vxreg = (P.decoders & GPD_DEC_VXLAN) != 0;
   // results of a finished tile, stored one iteration later
   bool st_pending = false;
   uint32_t st_i = 0, st_valid = 0;
@@ -1627,8 +1796,19 @@ __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
     if (cov_d && (P.options & kDiagSkipDecode)) {  // diagnostics: data movement only
       res = Out{g_lds[buf + ((off_d - Wd.base) & ~15u)], 0, 0, 0, 0, 0};
     } else if (cov_d) {
-      if (!fast_decode<CS, HASH, COOP>(buf + wshift(Wd) + (off_d - Wd.base), end_d - off_d, F, res, buf, sg))
+      if (HO) {
+        seg_pass<COOP>(buf + wshift(Wd) + (off_d - Wd.base), end_d - off_d, buf, hh, sg, F, vxreg);
+        got = 1;
+      } else if (!fast_decode<CS, HASH, COOP>(buf + wshift(Wd) + (off_d - Wd.base), end_d - off_d, F, res, buf, sg)) {
         fb = 1;
+      }
+    }
+    if (HO && __any(cov_d && hh.ok == 2u)) {  // VXLAN: decoded in full while its window is here
+      if (cov_d && hh.ok == 2u) {
+        got = 2;
+        if (!fast_decode<CS, HASH, COOP>(buf + wshift(Wd) + (off_d - Wd.base), end_d - off_d, F, res, buf, sg))
+          fb = 1;
+      }
     }
     {  // learn where this wave's network headers sit (mod 16) for the next windows' shift
       const uint32_t no = res.hoff & 0xFFFFu;
@@ -1642,13 +1822,19 @@ __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
         if (!pfx_done) window_prefix<STAGE>(buf, pfx, lane);
         if (sg.b > sg.a) {
           const uint32_t mid = lds_u32(pfx + 4u * sg.b) - lds_u32(pfx + 4u * sg.a);
-          res.csum |= fold_le_not(sg.part + mid) << 16;
+          if (HO && got == 1u) hh.sum = sg.part + mid;
+          else res.csum |= fold_le_not(sg.part + mid) << 16;
         }
       }
     }
     PH_MARK(3);  // cooperative checksum
     // ---- the tile is complete when the next window belongs to another tile (or none)
     if (!has_next || new_tile) {
+      if (HO && got == 1u) {  // the tile's one decode, from the staged headers
+        Seg none{0, 0, 0};
+        if (!fast_decode<CS, HASH, COOP, true>(0u, end_d - off_d, F, res, buf, none, &hh)) fb = 1;
+      }
+      got = 0;
       const uint64_t m = __ballot(fb != 0);  // the tile's leftovers go to the fallback list
       if (m) {
         uint32_t base = 0;
@@ -1726,7 +1912,7 @@ static hipError_t launch_t(const KParams &P, hipStream_t stream, int num_cus) {
   return hipGetLastError();
 }
 
-template <int STAGE, bool CS, bool HASH, int MINW, bool DEFER = false, bool RPFX = true>
+template <int STAGE, bool CS, bool HASH, int MINW, bool DEFER = false, bool RPFX = true, bool HO = false>
 static hipError_t launch_rs(const KParams &P, hipStream_t stream, int num_cus) {
   const uint64_t ntiles = (P.n + 63) / 64;
   const size_t lds = ((P.image_words * 4u + 15u) & ~15u) + 4 * (size_t)rs_wave_lds_bytes(STAGE) + 64;
@@ -1735,7 +1921,7 @@ static hipError_t launch_rs(const KParams &P, hipStream_t stream, int num_cus) {
   const uint64_t cap = (uint64_t)num_cus * per_cu * kGridRounds;  // rounds of resident workgroups
   if (blocks > cap) blocks = cap;
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL((rs_kernel<STAGE, CS, HASH, MINW, DEFER, RPFX>), dim3((unsigned)blocks), dim3(256), lds, stream, P);
+  hipLaunchKernelGGL((rs_kernel<STAGE, CS, HASH, MINW, DEFER, RPFX, HO>), dim3((unsigned)blocks), dim3(256), lds, stream, P);
   return hipGetLastError();
 }
 
@@ -1749,6 +1935,10 @@ static hipError_t launch_fast(const KParams &P, hipStream_t stream, int num_cus)
     if (P.waves == 2) return launch_rs<4096, CS, HASH, 2>(P, stream, num_cus);
     if (P.waves == 3) return launch_rs<4096, CS, HASH, 3>(P, stream, num_cus);
     return launch_rs<4096, CS, HASH, 4>(P, stream, num_cus);
+  }
+  if (P.options & kHeaderOnce) {
+    if (P.waves == 2) return launch_rs<8192, CS, HASH, 2, false, true, true>(P, stream, num_cus);
+    return launch_rs<8192, CS, HASH, 3, false, true, true>(P, stream, num_cus);
   }
   if (P.waves == 2) return launch_rs<8192, CS, HASH, 2>(P, stream, num_cus);
   if (P.options & kRegPrefix) return launch_rs<8192, CS, HASH, 3>(P, stream, num_cus);

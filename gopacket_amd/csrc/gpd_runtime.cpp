@@ -218,7 +218,7 @@ struct gpd_ctx {
     void *d = nullptr;
     size_t bytes = 0;
   } scratch[16];
-  gpd_tuning tune{0, -1, -1, 0};  // gpd_ctx_set_tuning (all automatic by default)
+  gpd_tuning tune{0, -1, -1, 0, -1};  // gpd_ctx_set_tuning (all automatic by default)
   bool timing = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, evm = nullptr;
   bool timed = false;
@@ -447,12 +447,13 @@ int gpd_last_launch_split(gpd_ctx *ctx, uint64_t *fallback, float *fast_ms, floa
 
 int gpd_ctx_set_tuning(gpd_ctx *ctx, const gpd_tuning *t) {
   if (!ctx) return set_err(GPD_ERR_INVALID, "gpd_ctx_set_tuning: null ctx");
-  const gpd_tuning automatic{0, -1, -1, 0};  // (waves_per_simd 0: automatic)
+  const gpd_tuning automatic{0, -1, -1, 0, -1};  // (waves_per_simd 0: automatic)
   if (!t) t = &automatic;
   if (t->window_bytes != 0 && t->window_bytes != 4096 && t->window_bytes != 8192)
     return set_err(GPD_ERR_INVALID, "gpd_ctx_set_tuning: window_bytes %u (0, 4096 or 8192)", t->window_bytes);
-  if (t->shift < -1 || t->shift > 1 || t->reg_prefix < -1 || t->reg_prefix > 1)
-    return set_err(GPD_ERR_INVALID, "gpd_ctx_set_tuning: shift / reg_prefix outside {-1, 0, 1}");
+  if (t->shift < -1 || t->shift > 1 || t->reg_prefix < -1 || t->reg_prefix > 1 || t->header_once < -1 ||
+      t->header_once > 1)
+    return set_err(GPD_ERR_INVALID, "gpd_ctx_set_tuning: shift / reg_prefix / header_once outside {-1, 0, 1}");
   if (t->waves_per_simd != 0 && (t->waves_per_simd < 2 || t->waves_per_simd > 4))
     return set_err(GPD_ERR_INVALID, "gpd_ctx_set_tuning: waves_per_simd %d (0, 2, 3 or 4)", t->waves_per_simd);
   ctx->tune = *t;
@@ -537,6 +538,11 @@ static int launch(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, hipS
   // the registers at commit
   if (ctx->tune.reg_prefix >= 0 ? ctx->tune.reg_prefix != 0 : (mean_slot > 160 && !shift))
     P.options |= 1u << 26;
+  // ... whose 64-packet tiles span several windows: decoded once per tile from the headers the
+  // windows stage (seg_pass), not once per window with the lanes each window holds
+  if (P.stage == 8192 &&
+      (ctx->tune.header_once >= 0 ? ctx->tune.header_once != 0 : (mean_slot > 160 && !shift)))
+    P.options |= 1u << 25;
   P.waves = (uint32_t)ctx->tune.waves_per_simd;
   P.nstores = 2u + (out->net_hash != nullptr) + (out->tp_hash != nullptr) + (out->csum != nullptr) +
               (out->hdr_off != nullptr);

@@ -46,8 +46,8 @@
 extern "C" {
 #endif
 
-#define GPD_ABI_VERSION 4  /* 2: ICMPv4 + LLC, 12 objects, 224-B ext; 3: gpd_result.hdr_off;
-                              4: gpd_ctx_set_tuning */
+#define GPD_ABI_VERSION 5  /* 2: ICMPv4 + LLC, 12 objects, 224-B ext; 3: gpd_result.hdr_off;
+                              4: gpd_ctx_set_tuning; 5: gpd_tuning.header_once */
 
 /* ---- gopacket LayerType numbers (layertypes.go:14-154, decode.go:105-116) ---- */
 #define GPD_LT_ZERO            0
@@ -325,6 +325,9 @@ typedef struct gpd_tuning {
                              -1 automatic (mean slot > 160 B), 0 off, 1 on */
   int32_t  waves_per_simd; /* resident waves of the fast kernel per SIMD: 0 automatic, 2, 3, 4
                               (4 KiB windows) or 2, 3 (8 KiB windows) */
+  int32_t  header_once;   /* 8 KiB windows: decode each 64-packet tile once from headers staged
+                             as its windows pass, instead of once per window: -1 automatic
+                             (mean slot > 160 B), 0 off, 1 on */
 } gpd_tuning;
 int  gpd_ctx_set_tuning(gpd_ctx *ctx, const gpd_tuning *t);
 const char *gpd_last_error_string(void);

@@ -201,6 +201,28 @@ def test_window_sizes_both_ways(window):
     run_both(PacketBatch.from_packets(_mutations(seed=29, per_packet=20)), ext=False, tuning=t)
 
 
+@pytest.mark.parametrize("extra", [{}, {"reg_prefix": 0}, {"shift": 1}, {"waves_per_simd": 2}],
+                         ids=["default", "lds_prefix", "shifted", "two_waves"])
+@pytest.mark.parametrize("ho", [0, 1])
+def test_header_once_both_ways(ho, extra):
+    """8 KiB windows decode a tile either once per window (the lanes each window holds) or
+    once per tile from the headers seg_pass staged in registers as the windows passed, with
+    the transport segment summed in its window (header_once).  Force each, over layouts whose
+    tiles span one window or several, TCP options (mutations), VXLAN (which the header-once
+    decode leaves to the generic decoder) and unaligned / pcap-like offsets."""
+    t = dict(window_bytes=8192, header_once=ho, **extra)
+    pk = _golden_packets()
+    run_both(PacketBatch.from_packets(pk), ext=False, tuning=t)
+    run_both(PacketBatch.from_packets(pk * 3, align=1), ext=False, tuning=t)
+    run_both(PacketBatch.from_packets(_mutations(seed=31, per_packet=40)), ext=False, tuning=t)
+    for maker in (synth.make_imix, synth.make_mixed, synth.make_traffic_mix, synth.make_vxlan,
+                  synth.make_udp64):
+        run_both(maker(1 << 13), ext=False, tuning=t)
+    from gopacket_amd import pcap as NP
+    cap = NP.synth_capture(synth.make_imix(1 << 12))
+    run_both(NP.index(cap).batch, ext=False, tuning=t)
+
+
 def test_layouts_unaligned_shuffled_large_empty():
     pk = _golden_packets() + [b"", b"\x01", b"\x00" * 13]
     big = [G.case_bytes(c) for c in CASES if c["name"] == "ipv6_jumbogram_dlp"][0]

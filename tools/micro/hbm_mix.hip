@@ -127,6 +127,57 @@ __global__ __launch_bounds__(256) void mix_lds_k(const v4u *__restrict__ in, uin
   }
 }
 
+// The same loop with the results written as MODE: 0 five SoA streams (the decode's layout),
+// 1 six SoA streams (+ a u32 hdr_off), 2 one AoS stream of 32-B records (two 16-B stores per
+// lane), 3 AoS 32-B records staged through LDS so each store instruction writes 1 KiB
+// contiguous (lane l writes bytes 16 l of the wave's 2 KiB of records).
+template <int MODE>
+__global__ __launch_bounds__(256) void mix_out_k(const v4u *__restrict__ in, uint32_t *st, uint64_t *ly,
+                                                uint64_t *nh, uint64_t *th, uint32_t *cs, uint32_t *ho,
+                                                v4u *rec, uint32_t ntiles, int work) {
+  __shared__ v4u lds[4][288];
+  __shared__ v4u orec[4][128];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t nw = gridDim.x * 4;
+  uint32_t t = blockIdx.x * 4 + wave;
+  v4u v[5];
+  auto load = [&](uint32_t tile) {
+    const v4u *p = in + (uint64_t)tile * 288;
+#pragma unroll
+    for (int k = 0; k < 4; k++) v[k] = __builtin_nontemporal_load(p + k * 64 + lane);
+    v[4] = lane < 32 ? __builtin_nontemporal_load(p + 256 + lane) : v4u{0u, 0u, 0u, 0u};
+  };
+  if (t < ntiles) load(t);
+  for (; t < ntiles; t += nw) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) lds[wave][k * 64 + lane] = v[k];
+    if (lane < 32) lds[wave][256 + lane] = v[4];
+    if (t + nw < ntiles) load(t + nw);
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    const v4u q = lds[wave][(lane * 4 + 3) % 288];
+    uint32_t x = q.x ^ q.y ^ q.z ^ q.w;
+    for (int r = 0; r < work; r++) x = x * 0x9E3779B1u + (x >> 7);
+    const uint64_t i = (uint64_t)t * 64 + lane;
+    if (MODE <= 1) {
+      __builtin_nontemporal_store(x, st + i);
+      __builtin_nontemporal_store((uint64_t)x * 3, ly + i);
+      __builtin_nontemporal_store((uint64_t)x * 5, nh + i);
+      __builtin_nontemporal_store((uint64_t)x * 7, th + i);
+      __builtin_nontemporal_store(x ^ 1u, cs + i);
+      if (MODE == 1) __builtin_nontemporal_store(x ^ 3u, ho + i);
+    } else if (MODE == 2) {
+      __builtin_nontemporal_store(v4u{x, x ^ 1u, x * 3u, 0u}, rec + 2 * i);
+      __builtin_nontemporal_store(v4u{x * 5u, 0u, x * 7u, 0u}, rec + 2 * i + 1);
+    } else {
+      orec[wave][2 * lane] = v4u{x, x ^ 1u, x * 3u, 0u};
+      orec[wave][2 * lane + 1] = v4u{x * 5u, 0u, x * 7u, 0u};
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_nontemporal_store(orec[wave][lane], rec + (uint64_t)t * 128 + lane);
+      __builtin_nontemporal_store(orec[wave][64 + lane], rec + (uint64_t)t * 128 + 64 + lane);
+    }
+  }
+}
+
 template <class F>
 static float time_ms(F f, int reps = 20) {
   hipEvent_t a, b;
@@ -188,6 +239,31 @@ int main() {
       const int g = cus * wpc;
       ms = time_ms([&] { hipLaunchKernelGGL(mix_lds_k, dim3(g), dim3(256), 0, 0, a, st, ly, nh, th, cs, ntiles, work); });
       printf("mixLDS work %3d wg/cu %2d       %.4f ms  %6.0f GB/s (r+w)  read %.0f\n", work, wpc, ms, (rd + wr) / ms / 1e6, rd / ms / 1e6);
+    }
+  }
+  uint32_t *ho;
+  v4u *rec;
+  CK(hipMalloc(&ho, 4ull << 24));
+  CK(hipMalloc(&rec, 32ull << 24));
+  const char *names[4] = {"SoA5", "SoA6", "AoS32", "AoS32lds"};
+  for (int wpc : {3, 4}) {
+    for (int work : {0, 64, 128}) {
+      for (int rep = 0; rep < 2; rep++) {
+        for (int mode = 0; mode < 4; mode++) {
+          const int g = cus * wpc;
+          auto f = [&] {
+            switch (mode) {
+              case 0: hipLaunchKernelGGL(mix_out_k<0>, dim3(g), dim3(256), 0, 0, a, st, ly, nh, th, cs, ho, rec, ntiles, work); break;
+              case 1: hipLaunchKernelGGL(mix_out_k<1>, dim3(g), dim3(256), 0, 0, a, st, ly, nh, th, cs, ho, rec, ntiles, work); break;
+              case 2: hipLaunchKernelGGL(mix_out_k<2>, dim3(g), dim3(256), 0, 0, a, st, ly, nh, th, cs, ho, rec, ntiles, work); break;
+              default: hipLaunchKernelGGL(mix_out_k<3>, dim3(g), dim3(256), 0, 0, a, st, ly, nh, th, cs, ho, rec, ntiles, work); break;
+            }
+          };
+          ms = time_ms(f);
+          const double w = mode == 1 ? 36.0 * (1 << 24) : wr;
+          printf("out %-8s work %3d wg/cu %d   %.4f ms  %6.0f GB/s (r+w)\n", names[mode], work, wpc, ms, (rd + w) / ms / 1e6);
+        }
+      }
     }
   }
   return 0;
