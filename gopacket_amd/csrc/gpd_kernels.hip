@@ -849,15 +849,14 @@ __device__ __forceinline__ void seg_pass(uint32_t p, uint32_t len, uint32_t buf,
   h.ok = 0;
   if (len < 15u) return;
   const U128 e = ld128(p + 8);
-  load64(h.W, p + 14);
   h.e1 = e.y;
   h.e2 = e.z;
   h.e3 = e.w;
   const uint32_t et0 = be_lo(e.y), et1 = be_lo(e.z);
-  if (et0 < 0x0600u) return;
   const uint32_t t1 = tag_type(et0), t2 = t1 & tag_type(et1);
   const uint32_t l3 = 14 + 4 * (t1 + t2);
-  if (t1) load64(h.W, p + l3);
+  load64(h.W, p + l3);  // one trip after the tags are known (no speculative untagged read)
+  if (et0 < 0x0600u) return;
   if (len < l3 + 20u) return;
   const uint32_t *W = h.W;
   const uint32_t ver = (W[0] >> 4) & 15u;
