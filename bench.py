@@ -218,12 +218,13 @@ def summarize(workload, n, world, steps, warmup, elapsed, kern_ms, kern_ms_max, 
     }
 
 
-def bench_record36(parser, dev_batch, n, local, stream, out, args):
+def bench_record36(parser, dev_batch, n, local, stream, out, args, records=False):
     """The same launch writing the 36-B record: the 32-B one plus hdr_off (the NetworkFlow /
-    TransportFlow header offsets the F3 flow table reads).  Event-timed like the metric."""
+    TransportFlow header offsets the F3 flow table reads).  Event-timed like the metric.
+    records=True: the 32-B record as one gpd_record per packet (AoS) instead of five arrays."""
     import torch
     from gopacket_amd import parser as P
-    res = P.DeviceResult(n, local, ext=False, hdr_off=True)
+    res = P.DeviceResult(n, local, ext=False, hdr_off=not records, records=records)
     for _ in range(3):
         parser.decode_device(dev_batch, res, stream)
     k = max(5, min(args.steps, 20))
@@ -235,9 +236,10 @@ def bench_record36(parser, dev_batch, n, local, stream, out, args):
     torch.cuda.synchronize(local)
     ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     rb = out["roofline"]["algorithmic_read_bytes"]
-    alg = rb + 36 * n
+    wb = 32 if records else 36
+    alg = rb + wb * n
     del res
-    return {"result_bytes_per_packet": 36, "kernel_ms": round(ms, 4),
+    return {"result_bytes_per_packet": wb, "kernel_ms": round(ms, 4),
             "Mpackets_per_s": round(n / ms / 1e3, 1),
             "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "read_frac": round(rb / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
@@ -930,6 +932,7 @@ def main():
                     batch, n_err, interleaved=16 if pcap_info else 0)
     if not args.ablate and not args.lean:  # the 36-B record (hdr_off on, as the flow table uses)
         out["record36"] = bench_record36(parser, dev_batch, n, local, stream, out, args)
+        out["record_aos"] = bench_record36(parser, dev_batch, n, local, stream, out, args, records=True)
         out["fallback"] = bench_split(parser, dev_batch, dev_res, n, local, stream)
     if pcap_info:
         out["pcap"] = pcap_info

@@ -53,6 +53,8 @@ constexpr uint32_t kDiagMask = kDiagSkipDecode | kDiagNoWait | kDiagNtLoad | kDi
 
 extern __shared__ __attribute__((aligned(16))) uint8_t g_lds[];
 
+typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+
 #ifdef GPD_PHASE_TIMING
 // Diagnostic build only (libgpd_phase.so): per-phase shader-clock totals of the fast kernel's
 // loop, summed over waves; read back with gpd_diag_phase().
@@ -1215,6 +1217,16 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 }
 
 __device__ __forceinline__ void store_out(const KParams &P, uint32_t i, const Out &o) {
+  if (P.rec) {  // one 32-B gpd_record: {status, csum, layers} and {net_hash, tp_hash}
+    v4u32 *r = reinterpret_cast<v4u32 *>(P.rec + i);
+    const v4u32 a = {o.status, o.csum, (uint32_t)o.layers, (uint32_t)(o.layers >> 32)};
+    const v4u32 b = {(uint32_t)o.net_hash, (uint32_t)(o.net_hash >> 32), (uint32_t)o.tp_hash,
+                     (uint32_t)(o.tp_hash >> 32)};
+    __builtin_nontemporal_store(a, r);
+    __builtin_nontemporal_store(b, r + 1);
+    if (P.hdr_off) __builtin_nontemporal_store(o.hoff, P.hdr_off + i);
+    return;
+  }
   if (P.options & kDiagNtStore) {
     __builtin_nontemporal_store(o.status, P.status + i);
     __builtin_nontemporal_store(o.layers, P.layers + i);
@@ -1556,7 +1568,6 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void decode_kernel(KParams P) {
 }
 
 // ---------------------------------------------------------------- register-staged fast loop
-typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
 
 // LDS bytes per wave of rs_kernel: one window (the next one waits in VGPRs), plus the chunk
 // prefix sums of the cooperative checksum for windows of 8 KiB and more.

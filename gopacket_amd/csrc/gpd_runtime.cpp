@@ -486,8 +486,12 @@ static int check_batch(const gpd_batch *in, const gpd_result *out) {
   if (in->n == 0) return GPD_OK;
   if (!in->data || !in->offset || !in->caplen)
     return set_err(GPD_ERR_INVALID, "gpd_decode: batch data/offset/caplen must be non-NULL");
-  if (!out->status || !out->layers)
+  if (out->records) {
+    if (out->status || out->layers || out->net_hash || out->tp_hash || out->csum)
+      return set_err(GPD_ERR_INVALID, "gpd_decode: records excludes the status/layers/net_hash/tp_hash/csum arrays");
+  } else if (!out->status || !out->layers) {
     return set_err(GPD_ERR_INVALID, "gpd_decode: result status/layers must be non-NULL");
+  }
   if ((reinterpret_cast<uintptr_t>(in->data) & 15) != 0)
     return set_err(GPD_ERR_INVALID, "gpd_decode: data pointer must be 16-byte aligned");
   if (in->data_len > 0xFFFFFFF0ull)
@@ -511,6 +515,7 @@ static int launch(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, hipS
   P.csum = out->csum;
   P.ext = out->ext;
   P.hdr_off = out->hdr_off;
+  P.rec = out->records;
   P.image = ctx->d_image;
   P.pages = ctx->d_pages;
   P.image_words = ctx->image_words;
@@ -544,8 +549,9 @@ static int launch(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, hipS
       (ctx->tune.header_once >= 0 ? ctx->tune.header_once != 0 : (mean_slot > 160 && !shift)))
     P.options |= 1u << 25;
   P.waves = (uint32_t)ctx->tune.waves_per_simd;
-  P.nstores = 2u + (out->net_hash != nullptr) + (out->tp_hash != nullptr) + (out->csum != nullptr) +
-              (out->hdr_off != nullptr);
+  P.nstores = out->records ? 2u + (out->hdr_off != nullptr)
+                           : 2u + (out->net_hash != nullptr) + (out->tp_hash != nullptr) +
+                                 (out->csum != nullptr) + (out->hdr_off != nullptr);
   if (gpd::fast_eligible(P)) {  // fallback list scratch for this stream, sized for one launch
     const uint64_t need = std::min<uint64_t>(in->n, gpd::kMaxLaunchPackets);
     auto &fb = ctx->fallback[stream];
@@ -572,8 +578,9 @@ static int launch(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, hipS
     Q.n = std::min<uint64_t>(gpd::kMaxLaunchPackets, in->n - lo);
     Q.offset = in->offset + lo;
     Q.caplen = in->caplen + lo;
-    Q.status = out->status + lo;
-    Q.layers = out->layers + lo;
+    Q.status = out->status ? out->status + lo : nullptr;
+    Q.layers = out->layers ? out->layers + lo : nullptr;
+    Q.rec = out->records ? out->records + lo : nullptr;
     Q.net_hash = out->net_hash ? out->net_hash + lo : nullptr;
     Q.tp_hash = out->tp_hash ? out->tp_hash + lo : nullptr;
     Q.csum = out->csum ? out->csum + lo : nullptr;

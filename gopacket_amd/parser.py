@@ -24,7 +24,7 @@ import numpy as np
 from . import layers as L
 from ._lib import GPD_ERR_PCAP, GpdBatch, GpdConfig, GpdResult, check, lib
 from .batch import PAD, PacketBatch
-from .results import EXT_DTYPE, BatchResult
+from .results import EXT_DTYPE, RECORD_DTYPE, BatchResult
 
 DEC_ETHERNET, DEC_DOT1Q, DEC_IPV4, DEC_IPV6, DEC_IPV6_EXT = 1, 2, 4, 8, 16
 DEC_TCP, DEC_UDP, DEC_VXLAN, DEC_PAYLOAD, DEC_FRAGMENT = 32, 64, 128, 256, 512
@@ -159,28 +159,40 @@ class DeviceBatch:
 
 
 class DeviceResult:
-    """Result SoA in HBM; .to_host() gives a BatchResult."""
+    """Results in HBM — the SoA arrays, or (records=True) one 32-B gpd_record per packet;
+    .to_host() gives a BatchResult either way."""
 
-    def __init__(self, n: int, device: int = 0, ext: bool = False, hdr_off: bool = True):
+    def __init__(self, n: int, device: int = 0, ext: bool = False, hdr_off: bool = True,
+                 records: bool = False):
         torch = _torch()
         dev = torch.device("cuda", device)
         self.n = n
-        self.status = torch.empty(n, dtype=torch.int32, device=dev)
-        self.layers = torch.empty(n, dtype=torch.int64, device=dev)
-        self.net_hash = torch.empty(n, dtype=torch.int64, device=dev)
-        self.tp_hash = torch.empty(n, dtype=torch.int64, device=dev)
-        self.csum = torch.empty(n, dtype=torch.int32, device=dev)
+        self.records = None
+        if records:
+            self.records = torch.empty(n * RECORD_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+            self.status = self.layers = self.net_hash = self.tp_hash = self.csum = None
+        else:
+            self.status = torch.empty(n, dtype=torch.int32, device=dev)
+            self.layers = torch.empty(n, dtype=torch.int64, device=dev)
+            self.net_hash = torch.empty(n, dtype=torch.int64, device=dev)
+            self.tp_hash = torch.empty(n, dtype=torch.int64, device=dev)
+            self.csum = torch.empty(n, dtype=torch.int32, device=dev)
         self.ext = torch.empty(n * EXT_DTYPE.itemsize, dtype=torch.uint8, device=dev) if ext else None
         self.hdr_off = torch.empty(n, dtype=torch.int32, device=dev) if hdr_off else None
 
     def c_result(self) -> GpdResult:
-        return GpdResult(self.status.data_ptr(), self.layers.data_ptr(), self.net_hash.data_ptr(),
-                         self.tp_hash.data_ptr(), self.csum.data_ptr(),
-                         self.ext.data_ptr() if self.ext is not None else None,
-                         self.hdr_off.data_ptr() if self.hdr_off is not None else None)
+        p = lambda t: t.data_ptr() if t is not None else None
+        return GpdResult(p(self.status), p(self.layers), p(self.net_hash), p(self.tp_hash),
+                         p(self.csum), p(self.ext), p(self.hdr_off), p(self.records))
 
     def to_host(self) -> BatchResult:
         u = lambda t, dt: t.cpu().numpy().view(dt)
+        if self.records is not None:
+            r = self.records.cpu().numpy().view(RECORD_DTYPE)
+            return BatchResult(r["status"].copy(), r["layers"].copy(), r["net_hash"].copy(),
+                               r["tp_hash"].copy(), r["csum"].copy(),
+                               self.ext.cpu().numpy().view(EXT_DTYPE) if self.ext is not None else None,
+                               u(self.hdr_off, np.uint32) if self.hdr_off is not None else None)
         return BatchResult(u(self.status, np.uint32), u(self.layers, np.uint64),
                            u(self.net_hash, np.uint64), u(self.tp_hash, np.uint64),
                            u(self.csum, np.uint32),

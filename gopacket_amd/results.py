@@ -21,6 +21,11 @@ OBJ_NAMES = ("Ethernet", "Dot1Q", "IPv4", "IPv6", "IPv6ExtensionSkipper", "TCP",
 
 LAYER_REC_DTYPE = np.dtype([("contents_off", "<u4"), ("contents_len", "<u4"),
                             ("payload_off", "<u4"), ("payload_len", "<u4")])
+# gpd_record (gpd.h): the AoS form of status, csum, layers, net_hash, tp_hash (32 B)
+RECORD_DTYPE = np.dtype([("status", "<u4"), ("csum", "<u4"), ("layers", "<u8"), ("net_hash", "<u8"),
+                         ("tp_hash", "<u8")])
+assert RECORD_DTYPE.itemsize == 32
+
 EXT_DTYPE = np.dtype([("layer_codes", "<u8", (2,)), ("err_arg0", "<u4"), ("err_arg1", "<u4"),
                       ("obj_valid", "<u2"), ("pad0", "<u2"), ("pad1", "<u4"),
                       ("obj", LAYER_REC_DTYPE, (12,))])

@@ -47,7 +47,8 @@ extern "C" {
 #endif
 
 #define GPD_ABI_VERSION 5  /* 2: ICMPv4 + LLC, 12 objects, 224-B ext; 3: gpd_result.hdr_off;
-                              4: gpd_ctx_set_tuning; 5: gpd_tuning.header_once */
+                              4: gpd_ctx_set_tuning; 5: gpd_tuning.header_once,
+                              gpd_result.records */
 
 /* ---- gopacket LayerType numbers (layertypes.go:14-154, decode.go:105-116) ---- */
 #define GPD_LT_ZERO            0
@@ -269,8 +270,22 @@ typedef struct gpd_batch {
 #define GPD_HDR_TP(h)  ((uint32_t)((h) >> 16))
 #define GPD_HDR_NONE   0xFFFFu
 
+/* One packet's five result words packed in 32 bytes (the AoS alternative to the SoA arrays). */
+typedef struct gpd_record {
+  uint32_t status;
+  uint32_t csum;
+  uint64_t layers;
+  uint64_t net_hash;
+  uint64_t tp_hash;
+} gpd_record;
+
 /* ---- results (caller-allocated SoA, n entries each) ----
- * status and layers are required; the others may be NULL (not written). */
+ * status and layers are required; the others may be NULL (not written).
+ * records (gpd_decode only): when non-NULL, status, layers, net_hash, tp_hash and csum must be
+ * NULL and each packet's five words are written as one 32-byte gpd_record instead (one
+ * stream of 2 x 16-byte stores per packet rather than five arrays); ext and hdr_off stay
+ * separate arrays.  The host-memory entry points (gpd_decode_host, gpd_decode_pcap*,
+ * TPACKET_V3) take the SoA form only. */
 typedef struct gpd_result {
   uint32_t    *status;
   uint64_t    *layers;
@@ -279,6 +294,7 @@ typedef struct gpd_result {
   uint32_t    *csum;
   gpd_ext_rec *ext;
   uint32_t    *hdr_off;    /* header offsets word (above) */
+  gpd_record  *records;    /* AoS form of the first five (see above) */
 } gpd_result;
 
 typedef struct gpd_ctx gpd_ctx;

@@ -58,14 +58,15 @@ def test_default_tables_match_reference_restatement():
 def test_struct_layouts_match_c(tmp_path):
     """sizeof/offsetof of the ABI structs as gcc sees them == the ctypes/numpy mirrors."""
     from gopacket_amd import _lib
-    from gopacket_amd.results import EXT_DTYPE
+    from gopacket_amd.results import EXT_DTYPE, RECORD_DTYPE
     prog = tmp_path / "sz.c"
     prog.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "gpd_pcap.h"\n#include "gpd_flow.h"\n'
                     'int main(void){'
-                    'printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(gpd_config), sizeof(gpd_batch),'
+                    'printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(gpd_config), sizeof(gpd_batch),'
                     ' sizeof(gpd_result), sizeof(gpd_ext_rec), offsetof(gpd_ext_rec, obj),'
                     ' sizeof(gpd_layer_rec), sizeof(gpd_pcap_info), sizeof(gpd_flow_rec),'
-                    ' offsetof(gpd_flow_rec, net_type), offsetof(gpd_flow_rec, first), sizeof(gpd_flow_stats));'
+                    ' offsetof(gpd_flow_rec, net_type), offsetof(gpd_flow_rec, first), sizeof(gpd_flow_stats),'
+                    ' sizeof(gpd_record), offsetof(gpd_record, layers), sizeof(gpd_tuning));'
                     ' return 0;}\n')
     exe = tmp_path / "sz"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(prog), "-o", str(exe)], check=True)
@@ -74,7 +75,8 @@ def test_struct_layouts_match_c(tmp_path):
     assert out == [C.sizeof(_lib.GpdConfig), C.sizeof(_lib.GpdBatch), C.sizeof(_lib.GpdResult),
                    EXT_DTYPE.itemsize, EXT_DTYPE.fields["obj"][1], 16, C.sizeof(_lib.GpdPcapInfo),
                    FLOW_REC_DTYPE.itemsize, FLOW_REC_DTYPE.fields["net_type"][1],
-                   FLOW_REC_DTYPE.fields["first"][1], C.sizeof(FlowStats)]
+                   FLOW_REC_DTYPE.fields["first"][1], C.sizeof(FlowStats),
+                   RECORD_DTYPE.itemsize, RECORD_DTYPE.fields["layers"][1], C.sizeof(_lib.GpdTuning)]
 
 
 @pytest.mark.skipif(gpu_available(), reason="checks the no-device error path")

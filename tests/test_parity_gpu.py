@@ -465,3 +465,37 @@ def test_host_paths_into_registered_result_arrays():
     finally:
         for a in arrs:
             lib.gpd_host_unregister(h, a.ctypes.data)
+
+
+def test_record_form_equals_soa():
+    """gpd_result.records (one 32-B gpd_record per packet) carries exactly the five SoA words,
+    through the fast kernel, its fallback list and the generic decoder (ext records), with
+    hdr_off beside it; a result naming both forms is refused."""
+    import ctypes as C
+    import torch
+    from gopacket_amd import parser as P
+    from gopacket_amd._lib import GPD_ERR_INVALID, GpdResult, lib
+    batches = [PacketBatch.from_packets(_golden_packets() * 3),
+               PacketBatch.from_packets(_mutations(seed=37, per_packet=40)),
+               synth.make_udp64(1 << 13), synth.make_imix(1 << 13), synth.make_vxlan(1 << 12),
+               synth.make_traffic_mix(1 << 13)]
+    for b in batches:
+        p = _parser()
+        db = P.DeviceBatch(b, 0)
+        for ext in (False, True):
+            soa = P.DeviceResult(b.n, 0, ext=ext, hdr_off=True)
+            aos = P.DeviceResult(b.n, 0, ext=ext, hdr_off=True, records=True)
+            p.decode_device(db, soa)
+            p.decode_device(db, aos)
+            torch.cuda.synchronize()
+            x, y = soa.to_host(), aos.to_host()
+            for f in ("status", "layers", "net_hash", "tp_hash", "csum", "hdr_off"):
+                assert np.array_equal(getattr(x, f), getattr(y, f)), (f, ext)
+            if ext:
+                assert np.array_equal(x.ext, y.ext)
+    soa, aos = P.DeviceResult(4, 0), P.DeviceResult(4, 0, records=True)
+    r = soa.c_result()
+    r.records = aos.records.data_ptr()
+    db = P.DeviceBatch(synth.make_udp64(4), 0)
+    rc = lib.gpd_decode(_parser().ctx().h, C.byref(db.c_batch()), C.byref(r), None)
+    assert rc == GPD_ERR_INVALID
