@@ -218,13 +218,14 @@ def summarize(workload, n, world, steps, warmup, elapsed, kern_ms, kern_ms_max, 
     }
 
 
-def bench_record36(parser, dev_batch, n, local, stream, out, args, records=False):
-    """The same launch writing the 36-B record: the 32-B one plus hdr_off (the NetworkFlow /
-    TransportFlow header offsets the F3 flow table reads).  Event-timed like the metric.
-    records=True: the 32-B record as one gpd_record per packet (AoS) instead of five arrays."""
+def bench_record36(parser, dev_batch, n, local, stream, out, args, records=False, soa=False):
+    """The same launch writing the 36-B record: the five SoA arrays plus hdr_off (the
+    NetworkFlow / TransportFlow header offsets the F3 flow table reads).  Event-timed like the
+    metric.  records=True: the 32-B record as one gpd_record per packet (AoS); soa=True: the
+    32-B record as the five SoA arrays."""
     import torch
     from gopacket_amd import parser as P
-    res = P.DeviceResult(n, local, ext=False, hdr_off=not records, records=records)
+    res = P.DeviceResult(n, local, ext=False, hdr_off=not (records or soa), records=records)
     for _ in range(3):
         parser.decode_device(dev_batch, res, stream)
     k = max(5, min(args.steps, 20))
@@ -236,7 +237,7 @@ def bench_record36(parser, dev_batch, n, local, stream, out, args, records=False
     torch.cuda.synchronize(local)
     ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     rb = out["roofline"]["algorithmic_read_bytes"]
-    wb = 32 if records else 36
+    wb = 32 if (records or soa) else 36
     alg = rb + wb * n
     del res
     return {"result_bytes_per_packet": wb, "kernel_ms": round(ms, 4),
@@ -484,16 +485,56 @@ def build_replay_capture(n: int, world: int, rank: int, local: int, key: str, di
 
 
 class _Res:
-    """Result SoA views (torch tensors, possibly slices of larger ones) as a gpd_result."""
+    """Result SoA views (torch tensors, possibly slices of larger ones) as a gpd_result, or
+    (records) a byte view of 32-B gpd_records."""
 
-    def __init__(self, status, layers, net_hash, tp_hash, csum):
+    def __init__(self, status=None, layers=None, net_hash=None, tp_hash=None, csum=None, records=None):
         self.status, self.layers, self.net_hash, self.tp_hash, self.csum = (
             status, layers, net_hash, tp_hash, csum)
+        self.records = records
 
     def c_result(self):
         from gopacket_amd._lib import GpdResult
+        if self.records is not None:
+            return GpdResult(None, None, None, None, None, None, None, self.records.data_ptr())
         return GpdResult(self.status.data_ptr(), self.layers.data_ptr(), self.net_hash.data_ptr(),
                          self.tp_hash.data_ptr(), self.csum.data_ptr(), None, None)
+
+    def fields(self, lo, hi):
+        """Host copies of the five result words of packets [lo, hi)."""
+        from gopacket_amd.results import RECORD_DTYPE
+        if self.records is not None:
+            r = self.records[32 * lo:32 * hi].cpu().numpy().view(RECORD_DTYPE)
+            return {f: r[f].copy() for f in ("status", "layers", "net_hash", "tp_hash", "csum")}
+        dt = {"status": np.uint32, "layers": np.uint64, "net_hash": np.uint64, "tp_hash": np.uint64,
+              "csum": np.uint32}
+        return {f: getattr(self, f)[lo:hi].cpu().numpy().view(d) for f, d in dt.items()}
+
+
+def settle(fn, ms, local):
+    """Run fn() (a launch of the timed step) untimed for >= ms of wall clock before the warmup
+    steps.  The GPU's clocks ramp up under sustained load over tens of milliseconds: measured on
+    one MI355X, config 2 ran at 0.354 ms per launch after 5 warmup launches and at 0.318-0.324 ms
+    after 300 or 1000 (same box, alternating runs), so a handful of warmup launches would time
+    the ramp rather than the steady state.  Returns the settle time spent (ms)."""
+    import torch
+    if ms <= 0:
+        return 0.0
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < ms:
+        for _ in range(8):
+            fn()
+        torch.cuda.synchronize(local)
+    return round((time.perf_counter() - t0) * 1e3, 1)
+
+
+def records_form(args) -> bool:
+    """The result form the line is timed with: one 32-B gpd_record per packet (AoS) for configs
+    2, 4 and 5, whose specs name no layout; the SoA arrays for IMIX (config 3 names "SoA
+    outputs", SURVEY.md §8(d)) and the traffic mix."""
+    if args.result_form != "auto":
+        return args.result_form == "aos"
+    return args.config not in ("imix", "mixed")
 
 
 def bench_replay(args, world, rank, local, dist):
@@ -559,9 +600,13 @@ def bench_replay(args, world, rank, local, dist):
     t0 = time.perf_counter()
     d_off = torch.empty(m, dtype=torch.int32, device=dev)
     d_len = torch.empty(m, dtype=torch.int32, device=dev)
-    res = _Res(torch.empty(m, dtype=torch.int32, device=dev), torch.empty(m, dtype=torch.int64, device=dev),
-               torch.empty(m, dtype=torch.int64, device=dev), torch.empty(m, dtype=torch.int64, device=dev),
-               torch.empty(m, dtype=torch.int32, device=dev))
+    aos = records_form(args)
+    if aos:
+        res = _Res(records=torch.empty(32 * m, dtype=torch.uint8, device=dev))
+    else:
+        res = _Res(torch.empty(m, dtype=torch.int32, device=dev), torch.empty(m, dtype=torch.int64, device=dev),
+                   torch.empty(m, dtype=torch.int64, device=dev), torch.empty(m, dtype=torch.int64, device=dev),
+                   torch.empty(m, dtype=torch.int32, device=dev))
     launches, read_bytes = [], 0
     for k, (a, b) in enumerate(chunks):
         hdr = int(cpos[k])
@@ -574,10 +619,10 @@ def bench_replay(args, world, rank, local, dist):
         d_len[a:b].copy_(torch.from_numpy(pc.batch.caplen.view(np.int32)))
         read_bytes += int(pc.batch.caplen.astype(np.int64).sum()) + (8 + 16) * (b - a)
         sl = slice(a, b)
+        part = (_Res(records=res.records[32 * a:32 * b]) if aos else
+                _Res(res.status[sl], res.layers[sl], res.net_hash[sl], res.tp_hash[sl], res.csum[sl]))
         launches.append((GpdBatch(d_bytes.data_ptr() + (base - base0), cend - base,
-                                  d_off[sl].data_ptr(), d_len[sl].data_ptr(), b - a),
-                         _Res(res.status[sl], res.layers[sl], res.net_hash[sl], res.tp_hash[sl],
-                              res.csum[sl]).c_result()))
+                                  d_off[sl].data_ptr(), d_len[sl].data_ptr(), b - a), part.c_result()))
     torch.cuda.synchronize(local)
     t_index = time.perf_counter() - t0
     stream = torch.cuda.current_stream(local)
@@ -587,6 +632,7 @@ def bench_replay(args, world, rank, local, dist):
         for b, r in launches:
             check(lib.gpd_decode(h, C.byref(b), C.byref(r), sp), "gpd_decode")
 
+    settled = settle(step, args.settle_ms, local)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(local)
@@ -605,7 +651,7 @@ def bench_replay(args, world, rank, local, dist):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([x.elapsed_time(y) for x, y in ev]))
-    st = res.status.cpu().numpy().view(np.uint32)
+    st = (res.records.view(torch.int32)[0::8] if aos else res.status).cpu().numpy().view(np.uint32)
     n_err = int(np.count_nonzero((st & 3) != 0))
     # PCIe-inclusive leg: the shard streamed from host memory in 2^24-record calls
     z = lambda dt: np.zeros(REPLAY_CHUNK, dt)
@@ -630,8 +676,8 @@ def bench_replay(args, world, rank, local, dist):
         dist.barrier()
     t_pcie = time.perf_counter() - t0
     # the streamed results of the last call equal the resident ones for the same records
-    same = all(np.array_equal(getattr(out, f)[:last],
-                              getattr(res, f)[m - last:m].cpu().numpy().view(getattr(out, f).dtype))
+    tail = res.fields(m - last, m)
+    same = all(np.array_equal(getattr(out, f)[:last], tail[f])
                for f in ("status", "layers", "net_hash", "tp_hash", "csum"))
     for a in outs:
         lib.gpd_host_unregister(h, a.ctypes.data)
@@ -675,6 +721,7 @@ def bench_replay(args, world, rank, local, dist):
                    "packets_total": n, "parallelism": f"shard{world}", "chunk_records": REPLAY_CHUNK,
                    "capture_bytes": dl, "capture_memory": "private" if world == 1 else "/dev/shm (shared)",
                    "read_bytes_per_packet": round(rb0 / m0, 2), "result_bytes_per_packet": write_per,
+                   "result_form": "gpd_record (AoS)" if aos else "SoA arrays", "settle_ms": settled,
                    "decode_errors": int(sum(r[5] for r in rows))},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
@@ -781,6 +828,12 @@ def main():
                     "(gpd_decode_tpv3, PCIe-inclusive); printed as a separate line")
     ap.add_argument("--decoders", default="all", choices=("all", "novxlan"),
                     help="registered decoders: all of the engine's set, or without VXLAN")
+    ap.add_argument("--settle-ms", type=float, default=250.0,
+                    help="untimed launches before the warmup steps, for at least this long (GPU "
+                         "clock ramp; 0: none)")
+    ap.add_argument("--result-form", default="auto", choices=("auto", "soa", "aos"),
+                    help="result form timed: auto = gpd_record (AoS) except for imix/mixed (SoA, as "
+                         "config 3 specifies)")
     ap.add_argument("--ablate", default="", help="diagnostics only: 'nocsum', 'nohash' or both "
                     "(comma separated); never used for the reported metric")
     ap.add_argument("--tune", default="", help="A/B only: engine tuning, e.g. 'shift=0' or "
@@ -845,7 +898,8 @@ def main():
                      "index_Mrec_per_s": round(n / t_index / 1e6, 1),
                      "index_threads": NP.last_walk_stats()[0]}
     dev_batch = P.DeviceBatch(batch, local)
-    dev_res = P.DeviceResult(n, local, ext=False, hdr_off=False)  # the 32-B record
+    aos = records_form(args)  # the 32-B record: gpd_record per packet, or the five SoA arrays
+    dev_res = P.DeviceResult(n, local, ext=False, hdr_off=False, records=aos)
     layers = [P.Ethernet(), P.Dot1Q(), P.IPv4(), P.IPv6(), P.IPv6ExtensionSkipper(), P.TCP(),
               P.UDP(), P.VXLAN(), P.Payload(), P.Fragment()]
     if args.decoders == "novxlan":
@@ -904,6 +958,7 @@ def main():
                   flush=True)
         return
 
+    settled = settle(lambda: parser.decode_device(dev_batch, dev_res, stream), args.settle_ms, local)
     for _ in range(args.warmup):
         parser.decode_device(dev_batch, dev_res, stream)
     torch.cuda.synchronize(local)
@@ -926,13 +981,18 @@ def main():
     elapsed, kern_ms_max = dist_max([elapsed, kern_ms], dist, f"cuda:{local}")
 
     # correctness guard on what was measured (cheap: status classes only)
-    st = dev_res.status.cpu().numpy().view(np.uint32)
+    st = (dev_res.records.view(torch.int32)[0::8] if aos else dev_res.status).cpu().numpy().view(np.uint32)
     n_err = int(np.count_nonzero((st & 3) != 0))
     out = summarize(workload, n, world, args.steps, args.warmup, elapsed, kern_ms, kern_ms_max,
                     batch, n_err, interleaved=16 if pcap_info else 0)
+    out["config"]["result_form"] = "gpd_record (AoS)" if aos else "SoA arrays"
+    out["config"]["settle_ms"] = settled
     if not args.ablate and not args.lean:  # the 36-B record (hdr_off on, as the flow table uses)
         out["record36"] = bench_record36(parser, dev_batch, n, local, stream, out, args)
-        out["record_aos"] = bench_record36(parser, dev_batch, n, local, stream, out, args, records=True)
+        if aos:  # the same launch writing the five SoA arrays
+            out["record_soa"] = bench_record36(parser, dev_batch, n, local, stream, out, args, soa=True)
+        else:
+            out["record_aos"] = bench_record36(parser, dev_batch, n, local, stream, out, args, records=True)
         out["fallback"] = bench_split(parser, dev_batch, dev_res, n, local, stream)
     if pcap_info:
         out["pcap"] = pcap_info
