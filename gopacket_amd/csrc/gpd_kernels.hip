@@ -793,6 +793,13 @@ __device__ __forceinline__ void window_prefix(uint32_t buf, uint32_t pfx, uint32
   if (lane == 63u) *reinterpret_cast<uint32_t *>(g_lds + pfx + 4u * K * 64u) = incl;
 }
 
+// TCP options the walk (tcp.go:274-300) accepts without reading them byte by byte: none, or
+// exactly NOP, NOP, Timestamps (kind 8, length 10) — what established connections carry.  w:
+// the first four option bytes (TCP header bytes 20..23) as a little-endian word.
+__device__ __forceinline__ bool tcp_opts_quick(uint32_t hl, uint32_t w) {
+  return hl == 20u || (hl == 32u && w == 0x0A080101u);
+}
+
 // Header-once decode (rs_kernel HO, windows of long frames): a tile of 64 such packets spans
 // several windows, and a straight-line decode per window would run with the few lanes whose
 // packets that window holds.  Instead, in the window that holds a packet, seg_pass keeps
@@ -892,7 +899,7 @@ __device__ __forceinline__ void seg_pass(uint32_t p, uint32_t len, uint32_t buf,
   if (g == 1u) {  // the options walk of fast_decode, on the guess
     const uint32_t hl = ((tw >> 4) & 15u) * 4u;
     uint32_t ok = (plen >= 20u && hl >= 20u && hl <= plen) ? 1u : 0u;
-    for (uint32_t q = 20; ok && q < hl;) {
+    for (uint32_t q = 20; ok && !tcp_opts_quick(hl, v4 ? W[10] : W[15]) && q < hl;) {
       const uint32_t k = g_lds[p + l4 + q];
       if (k == 0) break;
       uint32_t ol = 1;
@@ -1082,7 +1089,8 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
       hl = ((tw >> 4) & 15u) * 4u;
       if (plen < 20u || hl < 20u || hl > plen) return false;
       if (HO && !h->ok) return false;
-      for (uint32_t q = 20; !HO && q < hl;) {  // OPTIONS, tcp.go:274-300 (errors -> generic path)
+      // OPTIONS, tcp.go:274-300 (errors -> generic path)
+      for (uint32_t q = 20; !HO && !tcp_opts_quick(hl, v4 ? W[10] : W[15]) && q < hl;) {
         const uint32_t k = g_lds[p + l4 + q];
         if (k == 0) break;
         uint32_t ol = 1;
