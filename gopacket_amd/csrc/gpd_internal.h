@@ -105,51 +105,27 @@ void *ctx_scratch(gpd_ctx *ctx, int slot, size_t bytes);
 #include "../../include/gpd_pcap.h"
 #include <vector>
 namespace gpd {
-struct Recs {  // one walked stretch of records
-  std::vector<uint64_t> pos;  // record header positions
-  std::vector<uint32_t> cap, wire;
-  std::vector<uint64_t> ts;
-  bool lean = false;  // positions and capture lengths only (what a decode needs)
-  void reserve(size_t n) {
-    pos.reserve(n);
-    cap.reserve(n);
-    if (!lean) {
-      wire.reserve(n);
-      ts.reserve(n);
-    }
-  }
-  size_t size() const { return pos.size(); }
-  void clear() {  // keeps the capacity: a walk reused across calls touches no fresh pages
-    pos.clear();
-    cap.clear();
-    wire.clear();
-    ts.clear();
-  }
-  void push(uint64_t p, uint32_t c, uint32_t w, uint64_t t) {
-    pos.push_back(p);
-    cap.push_back(c);
-    if (!lean) {
-      wire.push_back(w);
-      ts.push_back(t);
-    }
-  }
+// Where a walk writes its records (any pointer may be NULL): record i's header position
+// pos64[i], its data offset off32[i] = pos + 16 - base, cap / wire / ts as ReadPacketData
+// returns them.
+struct PcapOut {
+  uint64_t base = 0;
+  uint32_t *off32 = nullptr;
+  uint64_t *pos64 = nullptr;
+  uint32_t *cap = nullptr, *wire = nullptr;
+  uint64_t *ts = nullptr;
 };
-struct PcapSlice {
-  size_t r, j0, cnt;  // records [j0, j0+cnt) of stretch r
+struct PcapResult {
+  uint64_t n = 0, next_pos = 0;  // records written; where the next record header starts
+  int stop = 0;                  // GPD_PCAP_STOP_*
+  uint32_t a0 = 0, a1 = 0;       // the stop's error arguments
+  bool off32_overflow = false;   // an off32 did not fit 32 bits
 };
-struct PcapWalk {
-  std::vector<Recs> R;          // per segment, then sequential re-walks
-  size_t used = 0;              // stretches of R in use (the rest keep their allocations)
-  bool lean = false;            // record positions and capture lengths only (Recs::lean)
-  std::vector<PcapSlice> plan;  // the walk, in order
-  uint64_t n = 0, next_pos = 0;
-  int stop = 0, threads = 0, met = 0, rewalks = 0;
-  uint32_t a0 = 0, a1 = 0;
-};
-int pcap_walk(const uint8_t *buf, uint64_t len, const gpd_pcap_info &I, uint64_t pos, uint64_t max_n,
-              int nthreads, PcapWalk &W);
-void pcap_emit(const PcapWalk &W, uint64_t base, uint32_t *off32, uint64_t *pos64, uint32_t *cap,
-               uint32_t *wire, uint64_t *ts);
+// The sequential ReadPacketData loop from pos, at most max_n records, into `out`; returns
+// GPD_OK or GPD_ERR_PCAP with the reference's error text (the records before the stop are
+// written and counted).
+int pcap_index_flat(const uint8_t *buf, uint64_t len, const gpd_pcap_info &I, uint64_t pos, uint64_t max_n,
+                    int nthreads, const PcapOut &out, PcapResult &R);
 int pcap_locate(const uint8_t *buf, uint64_t len, const gpd_pcap_info &I, uint64_t pos,
                 const uint64_t *targets, uint64_t k, uint64_t *pos_out, uint64_t *n_total, int *stop,
                 int nthreads);

@@ -16,7 +16,10 @@
 // so the speculative records from that position on are the true ones.  A segment whose
 // speculation the true walk never meets is re-walked sequentially.  The result is therefore
 // the sequential walk's for every input; speculation only decides how much of it runs in
-// parallel.
+// parallel.  Records are produced in two parallel passes over a window: the speculative
+// count (no stores), then — once the stitch has fixed where the true walk enters each segment
+// and how many of its records come before — a fill that writes every segment's records
+// straight into the caller's flat arrays at their final index.
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
@@ -86,25 +89,36 @@ inline int step(const uint8_t *buf, uint64_t len, const gpd_pcap_info &I, uint64
   return 1;
 }
 
-// Walk from p while record headers start before `limit`, at most max_n records.
-void walk(const uint8_t *buf, uint64_t len, const gpd_pcap_info &I, uint64_t p, uint64_t limit,
-          uint64_t max_n, Recs &out, End &e) {
+// Walk from p while record headers start before `limit`, at most max_n records, writing
+// record k of this walk at index at + k of `out`; returns the records written.
+uint64_t walk_store(const uint8_t *buf, uint64_t len, const gpd_pcap_info &I, uint64_t p, uint64_t limit,
+                uint64_t max_n, const PcapOut &out, uint64_t at, End &e, bool &overflow) {
   uint64_t n = 0;
+  const uint64_t d = GPD_PCAP_RECORD_BYTES - out.base;  // off32 = pos + 16 - base (mod 2^64)
   while (p < limit) {
     if (n == max_n) {
       e.stop = GPD_PCAP_STOP_LIMIT;
       e.pos = p;
       e.stopped = true;
-      return;
+      return n;
     }
     uint32_t cap, wire;
     uint64_t ts;
     if (!step(buf, len, I, p, cap, wire, ts, e)) {
       e.pos = p;
       e.stopped = true;
-      return;
+      return n;
     }
-    out.push(p, cap, wire, ts);
+    const uint64_t k = at + n;
+    if (out.off32) {
+      const uint64_t o = p + d;
+      overflow |= o >= (1ull << 32);
+      out.off32[k] = (uint32_t)o;
+    }
+    if (out.pos64) out.pos64[k] = p;
+    if (out.cap) out.cap[k] = cap;
+    if (out.wire) out.wire[k] = wire;
+    if (out.ts) out.ts[k] = ts;
     n++;
     p += GPD_PCAP_RECORD_BYTES + (uint64_t)cap;
     // the chain only moves forward through contiguous records: stream the bytes ahead of it
@@ -114,6 +128,7 @@ void walk(const uint8_t *buf, uint64_t len, const gpd_pcap_info &I, uint64_t p, 
   }
   e.pos = p;  // exit: the first record header at or past `limit`
   e.stopped = false;
+  return n;
 }
 
 // A header at x that, with the `depth` headers after it, passes every check of a record.
@@ -258,204 +273,167 @@ int pcap_locate(const uint8_t *buf, uint64_t len, const gpd_pcap_info &I, uint64
   return GPD_OK;
 }
 
-namespace {
-
-// Stretch r of the walk's record lists, cleared, its allocation kept (a reused walk touches no
-// fresh pages).
-Recs &stretch(PcapWalk &W, size_t r) {
-  if (W.R.size() <= r) W.R.resize(r + 1);
-  W.R[r].clear();
-  W.R[r].lean = W.lean;
-  return W.R[r];
-}
-
-// The true walk over the window buf[pos:end) appended to W's plan: the records whose headers
-// start before `end` (at most max_n when one thread walks the window), then the exit (the
-// first record header at or past `end`) or the stop.  With T > 1 threads the window is cut
-// into T segments; every segment but the first is walked speculatively from the first
-// position whose header chain looks like pcap records, and the segments are stitched in order.
-End walk_window(const uint8_t *buf, uint64_t len, const gpd_pcap_info &I, uint64_t pos, uint64_t end,
-                uint64_t max_n, int T, PcapWalk &W) {
-  const uint64_t span = end - pos;
-  std::vector<uint64_t> seg(T + 1);
-  for (int k = 0; k <= T; k++) seg[k] = pos + span * (uint64_t)k / (uint64_t)T;
-  const size_t r0 = W.used;
-  for (int k = 0; k < T; k++)
-    stretch(W, r0 + k).reserve((size_t)std::min<uint64_t>((seg[k + 1] - seg[k]) / 96 + 16, max_n + 16));
-  W.used += (size_t)T;
-  std::vector<End> E(T);
-  auto run = [&](int k) {
-    if (k == 0) {
-      walk(buf, len, I, pos, seg[1], T == 1 ? max_n : UINT64_MAX, W.R[r0], E[0]);
-      return;
-    }
-    // speculation: the first position of the segment that starts a plausible chain
-    const uint64_t hi = std::min<uint64_t>(seg[k + 1], seg[k] + GPD_PCAP_RECORD_BYTES + (uint64_t)I.snaplen + 1);
-    for (uint64_t x = seg[k]; x < hi; x++) {
-      if (plausible_chain(buf, len, I, x, 8)) {
-        walk(buf, len, I, x, seg[k + 1], UINT64_MAX, W.R[r0 + k], E[k]);
-        return;
-      }
-    }
-    E[k].stopped = false;
-    E[k].pos = UINT64_MAX;  // no speculation
-  };
+// Run f(k) for k in [0, T): k >= 1 on threads of their own, k = 0 on the caller's.
+template <class F>
+void par_segments(int T, F f) {
   if (T == 1) {
-    run(0);
-  } else {
-    std::vector<std::thread> th;
-    for (int k = 1; k < T; k++) th.emplace_back(run, k);
-    run(0);
-    for (auto &t : th) t.join();
+    f(0);
+    return;
   }
-  // stitch in order (no copies: the plan lists slices of the segment lists)
-  W.threads = std::max(W.threads, T);
-  W.plan.push_back(PcapSlice{r0, 0, W.R[r0].size()});
-  End cur = E[0];
-  for (int k = 1; k < T && !cur.stopped; k++) {
-    if (cur.pos >= seg[k + 1]) continue;  // no true record starts in segment k
-    const auto &P = W.R[r0 + k].pos;
-    auto it = std::lower_bound(P.begin(), P.end(), cur.pos);
-    if (it != P.end() && *it == cur.pos) {  // the true walk meets the speculation
-      const size_t j = (size_t)(it - P.begin());
-      W.plan.push_back(PcapSlice{r0 + (size_t)k, j, P.size() - j});
-      cur = E[k];
-      W.met++;
-    } else {  // it never does: walk this segment sequentially
-      const size_t r = W.used++;
-      End e;
-      walk(buf, len, I, cur.pos, seg[k + 1], UINT64_MAX, stretch(W, r), e);
-      W.plan.push_back(PcapSlice{r, 0, W.R[r].size()});
-      cur = e;
-      W.rewalks++;
-    }
-  }
-  return cur;
+  std::vector<std::thread> th;
+  th.reserve((size_t)T - 1);
+  for (int k = 1; k < T; k++) th.emplace_back(f, k);
+  f(0);
+  for (auto &t : th) t.join();
 }
 
-}  // namespace
-
-// The sequential walk's result over buf[pos:len) (see gpd_pcap.h), built in parallel: per
-// segment record lists plus the in-order plan of slices that make up the walk.
+// The sequential walk's result over buf[pos:len) (see gpd_pcap.h), built in parallel.
 //
-// An unbounded walk is one window over the whole buffer.  A bounded one (max_n records, e.g.
-// one chunk of a replay) must not read the whole buffer, so it goes window by window: the
-// first 256 records are walked sequentially to learn the mean record size, and each window
-// spans the bytes the records still missing would take at 1.25x that mean; windows are
-// walked in parallel like the whole buffer, and the walk continues from a window's exit
-// until it has max_n records or stops.  Windows only bound how far each step reads ahead:
-// the records and the stop are the sequential walk's.
-int pcap_walk(const uint8_t *buf, uint64_t len, const gpd_pcap_info &I, uint64_t pos, uint64_t max_n,
-              int nthreads, PcapWalk &W) {
-  W.used = 0;
-  W.plan.clear();
-  W.n = W.next_pos = 0;
-  W.stop = W.threads = W.met = W.rewalks = 0;
-  W.a0 = W.a1 = 0;
+// Window by window: the window is cut into segments; the count pass walks every segment
+// (segment 0 from the true position, bounded by the records still wanted; the others
+// speculatively) without storing; the stitch follows the true walk through the segments'
+// counts (re-counting a segment its speculation missed) and so knows, per segment, where the
+// true walk enters it and how many records precede it; the fill pass then walks each
+// segment's true records again and writes them at their final index.  An unbounded walk is
+// one window over the whole buffer.  A bounded one must not read the whole buffer: its first
+// 256 records are walked sequentially (learning the mean record size), and each later window
+// spans the bytes the records still missing would take at 1.1x that mean.  Windows only
+// bound how far each pass reads ahead: the records and the stop are the sequential walk's.
+int pcap_index_flat(const uint8_t *buf, uint64_t len, const gpd_pcap_info &I, uint64_t pos, uint64_t max_n,
+                    int nthreads, const PcapOut &out, PcapResult &R) {
+  R = PcapResult{};
   if (nthreads <= 0) nthreads = default_threads();
   const uint64_t kMinSeg = 4ull << 20;
+  const size_t kKeep = 4096;  // a speculation that syncs later than this is re-counted
   auto threads_for = [&](uint64_t span) {
     return (int)std::min<uint64_t>((uint64_t)nthreads, std::max<uint64_t>(1, span / kMinSeg));
   };
-  const uint64_t span = len > pos ? len - pos : 0;
+  int threads = 1, met = 0, rewalks = 0;
+  bool overflow = false;
   End cur;
-  uint64_t have = 0;  // records in the plan
-  if (max_n >= span / GPD_PCAP_RECORD_BYTES) {  // no bound short of the whole buffer
-    cur = walk_window(buf, len, I, pos, len, max_n, threads_for(span), W);
-    for (const auto &sl : W.plan) have += sl.cnt;
-  } else {
-    cur.pos = pos;
-    uint64_t p0 = pos;
-    bool first = true;
-    while (!cur.stopped && cur.pos < len && have < max_n) {
-      uint64_t end;
-      if (first) {  // learn the record sizes
-        end = len;
-        const size_t r = W.used++;
-        walk(buf, len, I, cur.pos, len, std::min<uint64_t>(256, max_n), stretch(W, r), cur);
-        W.plan.push_back(PcapSlice{r, 0, W.R[r].size()});
-        have += W.R[r].size();
-        if (cur.stopped && cur.stop == GPD_PCAP_STOP_LIMIT) cur.stopped = false;
-        first = false;
-        continue;
-      }
-      const double mean = have ? (double)(cur.pos - p0) / (double)have : 96.0;
-      const uint64_t want = (uint64_t)((double)(max_n - have) * mean * 1.25) + 4096;
-      end = std::min<uint64_t>(len, cur.pos + want);
-      cur = walk_window(buf, len, I, cur.pos, end, max_n - have, threads_for(end - cur.pos), W);
-      have = 0;
-      for (const auto &sl : W.plan) have += sl.cnt;
-      if (cur.stopped && cur.stop == GPD_PCAP_STOP_LIMIT) cur.stopped = false;
+  cur.pos = pos;
+  uint64_t have = 0;
+  const bool bounded = max_n < (len > pos ? len - pos : 0) / GPD_PCAP_RECORD_BYTES;
+  if (bounded) {  // learn the record sizes
+    have = walk_store(buf, len, I, pos, len, std::min<uint64_t>(256, max_n), out, 0, cur, overflow);
+    if (cur.stopped && cur.stop == GPD_PCAP_STOP_LIMIT) cur.stopped = false;
+  }
+  while (!cur.stopped && cur.pos < len && have < max_n) {
+    const uint64_t rem = max_n - have;
+    uint64_t end = len;
+    if (bounded) {
+      const double mean = have ? (double)(cur.pos - pos) / (double)have : 96.0;
+      end = std::min<uint64_t>(len, cur.pos + (uint64_t)((double)rem * mean * 1.1) + 65536);
     }
+    const int T = threads_for(end - cur.pos);
+    threads = std::max(threads, T);
+    if (T == 1) {  // one segment: a single storing pass
+      End e;
+      have += walk_store(buf, len, I, cur.pos, end, rem, out, have, e, overflow);
+      cur = e;
+      if (cur.stopped && cur.stop == GPD_PCAP_STOP_LIMIT && have < max_n) cur.stopped = false;
+      continue;
+    }
+    std::vector<uint64_t> seg(T + 1);
+    for (int k = 0; k <= T; k++) seg[k] = cur.pos + (end - cur.pos) * (uint64_t)k / (uint64_t)T;
+    // count pass
+    std::vector<Count> C(T);
+    par_segments(T, [&](int k) {
+      if (k == 0) {
+        count_walk(buf, len, I, cur.pos, seg[1], rem, 0, C[0]);
+        return;
+      }
+      const uint64_t hi = std::min<uint64_t>(seg[k + 1], seg[k] + GPD_PCAP_RECORD_BYTES + (uint64_t)I.snaplen + 1);
+      for (uint64_t x = seg[k]; x < hi; x++) {
+        if (plausible_chain(buf, len, I, x, 8)) {
+          count_walk(buf, len, I, x, seg[k + 1], UINT64_MAX, kKeep, C[k]);
+          return;
+        }
+      }
+      C[k].e.stopped = false;
+      C[k].e.pos = UINT64_MAX;  // no speculation
+    });
+    // stitch: where the true walk enters each segment, and its records there
+    std::vector<uint64_t> entry(T, 0), cnt(T, 0);
+    End e = C[0].e;
+    entry[0] = cur.pos;
+    cnt[0] = C[0].n;
+    uint64_t tot = cnt[0];
+    int used = 1;
+    for (int k = 1; k < T && !e.stopped && tot < rem; k++) {
+      entry[k] = e.pos;
+      used = k + 1;
+      if (e.pos >= seg[k + 1]) continue;  // no true record starts in segment k
+      const auto &F = C[k].first;
+      auto it = std::lower_bound(F.begin(), F.end(), e.pos);
+      if (it != F.end() && *it == e.pos) {  // the true walk meets the speculation
+        cnt[k] = C[k].n - (uint64_t)(it - F.begin());
+        e = C[k].e;
+        met++;
+      } else {  // it never does: count this segment from the true position
+        Count c;
+        count_walk(buf, len, I, e.pos, seg[k + 1], UINT64_MAX, 0, c);
+        cnt[k] = c.n;
+        e = c.e;
+        rewalks++;
+      }
+      tot += cnt[k];
+    }
+    bool trimmed = false;
+    if (tot > rem) {  // the bound falls inside segment used-1
+      cnt[used - 1] -= tot - rem;
+      tot = rem;
+      trimmed = true;
+    }
+    // fill pass: each segment's true records at their final index
+    std::vector<uint64_t> at(used + 1, have);
+    for (int k = 0; k < used; k++) at[k + 1] = at[k] + cnt[k];
+    std::vector<End> F(used);
+    std::vector<char> ovf(used, 0);
+    par_segments(used, [&](int k) {
+      bool o = false;
+      if (cnt[k]) walk_store(buf, len, I, entry[k], len, cnt[k], out, at[k], F[k], o);
+      ovf[k] = o;
+    });
+    for (int k = 0; k < used; k++) overflow |= ovf[k] != 0;
+    if (trimmed) {  // the walk continues right after the last record written
+      e = F[used - 1];
+      e.stop = GPD_PCAP_STOP_LIMIT;
+      e.stopped = true;
+    }
+    have += tot;
+    cur = e;
+    if (cur.stopped && cur.stop == GPD_PCAP_STOP_LIMIT && have < max_n) cur.stopped = false;
   }
   if (!cur.stopped && cur.pos >= len) {  // the walk reached the end: the next header starts exactly there
     cur.stop = GPD_PCAP_STOP_EOF;
     cur.stopped = true;
   }
-  uint64_t n = 0;
-  for (auto &sl : W.plan) {  // apply max_n
-    if (n + sl.cnt > max_n) {
-      sl.cnt = (size_t)(max_n - n);
-      const size_t at = (size_t)(&sl - W.plan.data());
-      cur.pos = W.R[sl.r].pos[sl.j0 + sl.cnt];
-      W.plan.resize(at + 1);
-      n = max_n;
-      break;
-    }
-    n += sl.cnt;
-  }
-  if (n == max_n) {  // as the sequential loop: the limit first
+  if (have == max_n) {  // as the sequential loop: the limit first
     cur.stop = GPD_PCAP_STOP_LIMIT;
     cur.a0 = cur.a1 = 0;
   }
-  W.n = n;
-  W.next_pos = cur.pos;
-  W.stop = cur.stop;
-  W.a0 = cur.a0;
-  W.a1 = cur.a1;
-  g_last_threads = W.threads;
-  g_last_met = W.met;
-  g_last_rewalks = W.rewalks;
-  switch (W.stop) {
+  R.n = have;
+  R.next_pos = cur.pos;
+  R.stop = cur.stop;
+  R.a0 = cur.a0;
+  R.a1 = cur.a1;
+  R.off32_overflow = overflow;
+  g_last_threads = threads;
+  g_last_met = met;
+  g_last_rewalks = rewalks;
+  switch (R.stop) {
     case GPD_PCAP_STOP_SHORT_HDR:
       return set_error(GPD_ERR_PCAP, "unexpected EOF");
     case GPD_PCAP_STOP_SNAPLEN:
-      return set_error(GPD_ERR_PCAP, "capture length exceeds snap length: %u > %u", W.a0, W.a1);
+      return set_error(GPD_ERR_PCAP, "capture length exceeds snap length: %u > %u", R.a0, R.a1);
     case GPD_PCAP_STOP_ORIGLEN:
-      return set_error(GPD_ERR_PCAP, "capture length exceeds original packet length: %u > %u", W.a0, W.a1);
+      return set_error(GPD_ERR_PCAP, "capture length exceeds original packet length: %u > %u", R.a0, R.a1);
     case GPD_PCAP_STOP_SHORT_DATA:
-      return set_error(GPD_ERR_PCAP, W.a0 == 0 ? "EOF" : "unexpected EOF");
+      return set_error(GPD_ERR_PCAP, R.a0 == 0 ? "EOF" : "unexpected EOF");
     default:
       return GPD_OK;
   }
-}
-
-// Copy the walk into flat arrays (any pointer may be NULL), one thread per slice.
-//   off32[i] = pos + 16 - base, pos64[i] = pos, cap / wire / ts as walked
-void pcap_emit(const PcapWalk &W, uint64_t base, uint32_t *off32, uint64_t *pos64, uint32_t *cap,
-               uint32_t *wire, uint64_t *ts) {
-  std::vector<uint64_t> at(W.plan.size() + 1, 0);
-  for (size_t s = 0; s < W.plan.size(); s++) at[s + 1] = at[s] + W.plan[s].cnt;
-  auto one = [&](size_t s) {
-    const PcapSlice &sl = W.plan[s];
-    const Recs &r = W.R[sl.r];
-    const uint64_t o = at[s];
-    const uint64_t d = GPD_PCAP_RECORD_BYTES - base;  // wraps, as unsigned arithmetic intends
-    if (off32)
-      for (size_t j = 0; j < sl.cnt; j++) off32[o + j] = (uint32_t)(r.pos[sl.j0 + j] + d);
-    if (pos64) std::memcpy(pos64 + o, r.pos.data() + sl.j0, sl.cnt * 8);
-    if (cap) std::memcpy(cap + o, r.cap.data() + sl.j0, sl.cnt * 4);
-    if (wire && !r.lean) std::memcpy(wire + o, r.wire.data() + sl.j0, sl.cnt * 4);
-    if (ts && !r.lean) std::memcpy(ts + o, r.ts.data() + sl.j0, sl.cnt * 8);
-  };
-  if (W.plan.size() <= 1) {
-    if (!W.plan.empty()) one(0);
-    return;
-  }
-  std::vector<std::thread> th;
-  for (size_t s = 1; s < W.plan.size(); s++) th.emplace_back(one, s);
-  one(0);
-  for (auto &t : th) t.join();
 }
 
 }  // namespace gpd
@@ -502,18 +480,18 @@ int gpd_pcap_index(const uint8_t *buf, uint64_t len, const gpd_pcap_info *info, 
   if (!info || !n_out || (!buf && len) || (max_n && (!offset || !caplen)))
     return gpd::set_error(GPD_ERR_INVALID, "gpd_pcap_index: null argument");
   if (pos > len) return gpd::set_error(GPD_ERR_INVALID, "gpd_pcap_index: pos beyond the buffer");
-  gpd::PcapWalk W;
-  const int rc = gpd::pcap_walk(buf, len, *info, pos, max_n, nthreads, W);
-  if (W.n) {
-    const auto &last = W.plan.back();
-    if (W.R[last.r].pos[last.j0 + last.cnt - 1] + GPD_PCAP_RECORD_BYTES >= (1ull << 32))
-      return gpd::set_error(GPD_ERR_INVALID,
-                            "gpd_pcap_index: record offsets beyond 4 GiB; index the capture in windows");
-  }
-  gpd::pcap_emit(W, 0, offset, nullptr, caplen, wirelen, ts_ns);
-  *n_out = W.n;
-  if (next_pos) *next_pos = W.next_pos;
-  if (stop) *stop = W.stop;
+  gpd::PcapOut o;
+  o.off32 = offset;
+  o.cap = caplen;
+  o.wire = wirelen;
+  o.ts = ts_ns;
+  gpd::PcapResult R;
+  const int rc = gpd::pcap_index_flat(buf, len, *info, pos, max_n, nthreads, o, R);
+  if (R.off32_overflow)
+    return gpd::set_error(GPD_ERR_INVALID, "gpd_pcap_index: record offsets beyond 4 GiB; index the capture in windows");
+  *n_out = R.n;
+  if (next_pos) *next_pos = R.next_pos;
+  if (stop) *stop = R.stop;
   return rc;
 }
 

@@ -882,15 +882,17 @@ int gpd_decode_pcap_at(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, const gpd
   if (max_n == 0) return GPD_OK;
   HIP_TRY(hipSetDevice(ctx->device));
   const uint64_t kPkts = 1u << 20, kBytes = 256ull << 20;
+  const uint64_t kPart = 1u << 21;  // records per walked part (the first, walked before any
+  const uint64_t kPart0 = 1u << 19; // transfer can start, is smaller)
   int rc = alloc_slots(ctx, kBytes, kPkts, false);
   if (rc) return rc;
   SlotGuard guard{ctx};
-  // The record walk runs one part (kPkts records) ahead of the transfers, on a helper thread:
-  // while part q's chunks travel and decode, part q+1 is walked.  Two parts' walks and their
-  // flattened positions are kept per calling thread across calls (a replay or capture loop
-  // calls again and again; fresh pages for 24 B per record cost more than the walk itself).
+  // The record walk runs one part (kPart records) ahead of the transfers, on a helper thread:
+  // while part q's chunks travel and decode, part q+1 is walked.  Two parts' record positions
+  // and capture lengths are kept per calling thread across calls (a replay or capture loop
+  // calls again and again; fresh pages for 12 B per record would cost more than the walk).
   struct Part {
-    gpd::PcapWalk W;
+    gpd::PcapResult W;
     std::vector<uint64_t> rp;
     std::vector<uint32_t> rcap;
     int rc = 0;
@@ -902,19 +904,20 @@ int gpd_decode_pcap_at(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, const gpd
   double walk_ms = 0;  // (written by the walking thread, read after its join)
   auto walk_part = [&](Part &P, uint64_t at, uint64_t m) {
     const double t0 = now_ms();
-    P.W.lean = true;  // positions and capture lengths only
-    P.rc = gpd::pcap_walk(buf, len, *info, at, m, nthreads, P.W);
-    P.err = P.rc ? std::string(gpd_last_error_string()) : std::string();  // (the walker's thread)
-    if (P.rp.size() < P.W.n) {
-      P.rp.resize(P.W.n);
-      P.rcap.resize(P.W.n);
+    if (P.rp.size() < m) {
+      P.rp.resize(m);
+      P.rcap.resize(m);
     }
-    gpd::pcap_emit(P.W, 0, nullptr, P.rp.data(), P.rcap.data(), nullptr, nullptr);
+    gpd::PcapOut o;  // positions and capture lengths only (what a decode needs)
+    o.pos64 = P.rp.data();
+    o.cap = P.rcap.data();
+    P.rc = gpd::pcap_index_flat(buf, len, *info, at, m, nthreads, o, P.W);
+    P.err = P.rc ? std::string(gpd_last_error_string()) : std::string();  // (the walker's thread)
     walk_ms += now_ms() - t0;
   };
   uint64_t done = 0;  // records decoded (the output index of the next one)
   int q = 0;
-  walk_part(part[0], pos, std::min(kPkts, max_n));
+  walk_part(part[0], pos, std::min(kPart0, max_n));
   struct Joiner {  // every exit, errors included, waits for the walk running ahead
     std::thread t;
     ~Joiner() {
@@ -927,7 +930,7 @@ int gpd_decode_pcap_at(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, const gpd
     const uint64_t n = cur.W.n;
     const bool more = cur.rc == GPD_OK && cur.W.stop == GPD_PCAP_STOP_LIMIT && n > 0 && done + n < max_n;
     if (more)  // walk the next part while this one is staged
-      ahead.t = std::thread(walk_part, std::ref(part[q ^ 1]), cur.W.next_pos, std::min(kPkts, max_n - done - n));
+      ahead.t = std::thread(walk_part, std::ref(part[q ^ 1]), cur.W.next_pos, std::min(kPart, max_n - done - n));
     uint64_t i = 0;
     while (i < n) {
       auto &s = ctx->slot[k];
