@@ -168,12 +168,15 @@ def load_traffic(config: str):
             "source": os.path.relpath(paths[-1], ROOT)}
 
 
+COMM_DEVICE = None  # where collective operands live: the rank's GPU (nccl) or "cpu" (gloo)
+
+
 def dist_max(values, dist, device):
     """Max over ranks of a few floats (identity without torch.distributed)."""
     if not dist:
         return [float(v) for v in values]
     import torch
-    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=COMM_DEVICE or device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return [float(v) for v in t.cpu()]
 
@@ -552,7 +555,8 @@ def bench_replay(args, world, rank, local, dist):
     threads = args.threads or 16
     key = f"{REPLAY_SEED:x}_{n}_{os.environ.get('MASTER_PORT', '0')}"
     t0 = time.perf_counter()
-    cap, mm = build_replay_capture(n, world, rank, local, key, dist, threads)
+    host_local = int(os.environ.get("LOCAL_RANK", local))  # the host roles (--same-device keeps them)
+    cap, mm = build_replay_capture(n, world, rank, host_local, key, dist, threads)
     t_gen = time.perf_counter() - t0
     dl = 24 + 80 * n
     info = NP.header(cap, dl)
@@ -566,7 +570,7 @@ def bench_replay(args, world, rank, local, dist):
     else:
         pos = np.zeros(world + 1, np.uint64)
     if dist:
-        pt = torch.from_numpy(pos.view(np.int64).copy()).to(dev)
+        pt = torch.from_numpy(pos.view(np.int64).copy()).to(COMM_DEVICE or dev)
         dist.broadcast(pt, 0)
         pos = pt.cpu().numpy().view(np.uint64)
     start, end = int(pos[rank]), int(pos[rank + 1])
@@ -688,7 +692,7 @@ def bench_replay(args, world, rank, local, dist):
             t_gen, t_locate, t_reg, t_h2d, t_index, float(registered)]
     rows = [mine]
     if dist:
-        t = torch.tensor(mine, dtype=torch.float64, device=dev)
+        t = torch.tensor(mine, dtype=torch.float64, device=COMM_DEVICE or dev)
         g = [torch.zeros_like(t) for _ in range(world)]
         dist.all_gather(g, t)
         rows = [list(x.cpu().numpy()) for x in g]
@@ -753,7 +757,8 @@ def shard_check(args, world, rank, local, dist):
     n = args.packets or 10 ** 9
     threads = args.threads or 4
     key = f"{REPLAY_SEED:x}_{n}_{os.environ.get('MASTER_PORT', '0')}"
-    cap, mm = build_replay_capture(n, world, rank, local, key, dist, threads)
+    host_local = int(os.environ.get("LOCAL_RANK", local))  # the host roles (--same-device keeps them)
+    cap, mm = build_replay_capture(n, world, rank, host_local, key, dist, threads)
     dl = 24 + 80 * n
     info = NP.header(cap, dl)
     bounds = NP.shard_bounds(n, world)
@@ -841,6 +846,10 @@ def main():
     ap.add_argument("--shard-check", default="", help="tests only (CPU, gloo): build the replay "
                     "capture, cut and index this rank's shard, write its record positions to DIR")
     ap.add_argument("--chunk", type=int, default=0, help="tests only: records per index chunk")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="tests only: gloo rehearses the N-rank path without RCCL")
+    ap.add_argument("--same-device", action="store_true",
+                    help="tests only: every rank on cuda:0 (the N-rank path on a one-GPU box, gloo)")
     ap.add_argument("--lean", action="store_true", help="only the timed launches (profiling runs: "
                     "no 36-B record line, no fallback split, no CPU baseline)")
     args = ap.parse_args()
@@ -852,7 +861,9 @@ def main():
     if args.gpus is not None and args.gpus != world:
         raise SystemExit(f"bench: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", "0"))
+    if args.same_device and args.dist_backend != "gloo":
+        raise SystemExit("bench: --same-device needs --dist-backend gloo (RCCL wants a GPU per rank)")
 
     import torch
     dist = None
@@ -864,10 +875,15 @@ def main():
         if dist:
             dist.destroy_process_group()
         return
+    global COMM_DEVICE
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "gloo":
+            dist.init_process_group("gloo")
+            COMM_DEVICE = "cpu"
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(local)
 
