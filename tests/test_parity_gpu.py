@@ -499,3 +499,33 @@ def test_record_form_equals_soa():
     db = P.DeviceBatch(synth.make_udp64(4), 0)
     rc = lib.gpd_decode(_parser().ctx().h, C.byref(db.c_batch()), C.byref(r), None)
     assert rc == GPD_ERR_INVALID
+
+
+@pytest.mark.parametrize("ho", [0, 1])
+def test_long_frame_mutations_both_ways(ho):
+    """Long frames (a header-once batch: 8 KiB windows, tiles spanning several) with their
+    headers fuzzed — EtherType and tags, IPv4 version/IHL/length/flags/protocol, TCP data
+    offset and option bytes (the Timestamps shortcut's pattern among them), UDP length — and
+    cut at random lengths, mixed among intact IMIX frames, against the oracle with
+    header-once forced off and on."""
+    rng = np.random.default_rng(41 + ho)
+    base = synth.make_imix(1 << 12)
+    n = base.n
+    data = base.data.copy()
+    offs, lens = base.offset.astype(np.int64), base.caplen.astype(np.int64).copy()
+    hot = (12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 24, 25, 27, 28, 31, 50, 51, 58, 59, 60, 61, 62, 63, 64, 65)
+    for i in rng.choice(n, size=n // 2, replace=False):
+        o = int(offs[i])
+        for _ in range(int(rng.integers(1, 4))):
+            k = int(rng.choice(hot)) if rng.random() < 0.8 else int(rng.integers(0, min(128, lens[i])))
+            if k < lens[i]:
+                data[o + k] = rng.integers(0, 256)
+        if rng.random() < 0.2:
+            lens[i] = int(rng.integers(0, lens[i] + 1))
+        if rng.random() < 0.1 and lens[i] >= 70:  # NOP NOP Timestamps on a 32-B TCP header
+            data[o + 18 + 20 + 12] = 0x80
+            data[o + 58:o + 62] = (1, 1, 8, 10)
+    b = PacketBatch(data, base.data_len, base.offset.copy(), lens.astype(np.uint32))
+    t = dict(window_bytes=8192, header_once=ho)
+    run_both(b, ext=False, tuning=t)
+    run_both(b, L.LayerTypeEthernet, 0x3FF, ext=False, tuning=t)
