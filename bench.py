@@ -738,8 +738,9 @@ def bench_replay(args, world, rank, local, dist):
         "pcie_inclusive": {"Mpackets_per_s": round(n / pcie_max / 1e6, 1), "s": round(pcie_max, 3),
                            "GBps_capture_in": round(dl / pcie_max / 1e9, 2),
                            "path": "registered shared capture -> gpd_decode_pcap_at per 2^24 records "
-                                   "(record walk one part ahead, raw bytes H2D, decode, results "
-                                   "D2H into registered result arrays)"},
+                                   "(raw bytes H2D in 64 MiB chunks, records found in HBM by the "
+                                   "device walk, decode, results D2H into registered result "
+                                   "arrays)"},
         "per_rank": per_rank,
         "setup_s": {"generate": round(rows[0][7], 2), "locate": round(rows[0][8], 2),
                     "register": round(rows[0][9], 2), "h2d": round(rows[0][10], 2),

@@ -51,6 +51,7 @@ struct KParams {
   const uint32_t *offset;
   const uint32_t *caplen;
   uint64_t n;
+  const uint32_t *n_dev;       // when set, the packet count is min(n, *n_dev), read on the device
   uint32_t *status;
   uint64_t *layers;
   uint64_t *net_hash;
@@ -81,6 +82,29 @@ struct KParams {
 // True when launch_decode takes the fast kernel + fallback list (needs fb_count/fb_list
 // with room for P.n entries).
 bool fast_eligible(const KParams &P);
+
+// The pcap record walk on the GPU (gpd_pcapwalk.hip): one chunk of capture bytes in HBM.
+constexpr uint32_t kPwSeg = 2048;        // bytes per walking lane
+constexpr uint32_t kPwMaxSeg = 1u << 15; // segments per chunk (64 MiB)
+struct PwCtl {       // a chunk's control block (device; copied back to the host)
+  uint32_t entry;    // in: its first record header (relative to the chunk)
+  uint32_t n;        // out: records whose headers start in [entry, own_end)
+  uint32_t next;     // out: the first record header at or past own_end
+  uint32_t status;   // out: 0, or 1 = the host walks from `entry` (see gpd_pcapwalk.hip)
+};
+struct PwArgs {
+  const uint8_t *d;        // the chunk's bytes in HBM
+  uint32_t T;              // bytes there
+  uint32_t own_end;        // records whose headers start before this are the chunk's
+  uint32_t nseg;           // ceil(own_end / kPwSeg)
+  uint32_t snaplen;
+  bool be, nano, last;     // header byte order, ns timestamps; the chunk ends the capture (T = its end)
+  PwCtl *ctl, *ctl_next;   // this chunk's block; the next chunk's (its entry is written)
+  uint32_t *st, *ex, *ct, *bad, *base;  // per segment
+  uint32_t *off, *len;     // per record: data offset, capture length
+};
+hipError_t launch_pcap_walk(const PwArgs &A, hipStream_t stream);
+hipError_t launch_pcap_fill(const PwArgs &A, hipStream_t stream);
 
 // One launch covers at most this many packets, so packet and tile indices are 32-bit.
 constexpr uint64_t kMaxLaunchPackets = 1ull << 30;

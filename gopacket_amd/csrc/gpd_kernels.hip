@@ -1403,7 +1403,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void decode_kernel(KParams P) {
   const uint32_t bufs = img + wave * wave_lds_bytes(STAGE, FAST);
   const uint32_t dslots = bufs + 2u * STAGE;  // two slots of 64 offsets + 64 caplens
   const uint32_t pfx = dslots + 1024u;        // COOP: 513 chunk prefix sums
-  const uint32_t n = (uint32_t)P.n;  // <= kMaxLaunchPackets per launch
+  const uint32_t n = P.n_dev ? min((uint32_t)P.n, *P.n_dev) : (uint32_t)P.n;  // <= kMaxLaunchPackets
   const uint32_t ntiles = (n + 63u) >> 6;
   const uint32_t nwaves = gridDim.x * WAVES;
   const uint32_t dlen = (uint32_t)P.data_len;
@@ -1660,7 +1660,7 @@ __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
   const uint32_t img = (P.image_words * 4u + 15u) & ~15u;
   const uint32_t buf = img + wave * rs_wave_lds_bytes(STAGE);
   const uint32_t pfx = buf + STAGE + 16u;
-  const uint32_t n = (uint32_t)P.n;
+  const uint32_t n = P.n_dev ? min((uint32_t)P.n, *P.n_dev) : (uint32_t)P.n;
   const uint32_t ntiles = (n + 63u) >> 6;
   const uint32_t nwaves = gridDim.x * WAVES;
   const uint32_t dlen = (uint32_t)P.data_len;

@@ -218,7 +218,7 @@ struct gpd_ctx {
     void *d = nullptr;
     size_t bytes = 0;
   } scratch[16];
-  gpd_tuning tune{0, -1, -1, 0, -1};  // gpd_ctx_set_tuning (all automatic by default)
+  gpd_tuning tune{0, -1, -1, 0, -1, -1};  // gpd_ctx_set_tuning (all automatic by default)
   bool timing = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, evm = nullptr;
   bool timed = false;
@@ -234,11 +234,14 @@ struct gpd_ctx {
     uint64_t *h_th = nullptr, *d_th = nullptr;
     uint32_t *h_hoff = nullptr, *d_hoff = nullptr;
     gpd_ext_rec *h_ext = nullptr, *d_ext = nullptr;
+    uint32_t *d_pw = nullptr;  // the device pcap walk's per-segment arrays (5 x kPwMaxSeg)
     uint64_t lo = 0, hi = 0;  // packet range in flight
     bool busy = false;
     bool direct = false;      // its results go straight into the caller's (registered) arrays
   } slot[2];
   uint64_t slot_bytes = 0, slot_pkts = 0;
+  gpd::PwCtl *d_pw_ctl = nullptr, *h_pw_ctl = nullptr;  // one control block per slot
+  hipEvent_t ev_pw[2] = {nullptr, nullptr};            // a slot's chunk walked (and its block read back)
   // host ranges pinned with gpd_host_register (H2D reads them in place)
   std::vector<std::pair<const uint8_t *, uint64_t>> registered;
   bool is_registered(const uint8_t *p, uint64_t n) const {
@@ -403,11 +406,17 @@ static void free_slots(gpd_ctx *ctx) {
       if (p) (void)hipHostFree(p);
     for (void *p : {(void *)s.d_data, (void *)s.d_off, (void *)s.d_len, (void *)s.d_status,
                     (void *)s.d_csum, (void *)s.d_layers, (void *)s.d_nh, (void *)s.d_th,
-                    (void *)s.d_hoff, (void *)s.d_ext})
+                    (void *)s.d_hoff, (void *)s.d_ext, (void *)s.d_pw})
       if (p) (void)hipFree(p);
     if (s.stream) (void)hipStreamDestroy(s.stream);
     s = gpd_ctx::Slot{};
   }
+  if (ctx->d_pw_ctl) (void)hipFree(ctx->d_pw_ctl);
+  if (ctx->h_pw_ctl) (void)hipHostFree(ctx->h_pw_ctl);
+  for (auto &e : ctx->ev_pw)
+    if (e) (void)hipEventDestroy(e);
+  ctx->d_pw_ctl = ctx->h_pw_ctl = nullptr;
+  ctx->ev_pw[0] = ctx->ev_pw[1] = nullptr;
   ctx->slot_bytes = ctx->slot_pkts = 0;
 }
 
@@ -447,13 +456,14 @@ int gpd_last_launch_split(gpd_ctx *ctx, uint64_t *fallback, float *fast_ms, floa
 
 int gpd_ctx_set_tuning(gpd_ctx *ctx, const gpd_tuning *t) {
   if (!ctx) return set_err(GPD_ERR_INVALID, "gpd_ctx_set_tuning: null ctx");
-  const gpd_tuning automatic{0, -1, -1, 0, -1};  // (waves_per_simd 0: automatic)
+  const gpd_tuning automatic{0, -1, -1, 0, -1, -1};  // (waves_per_simd 0: automatic)
   if (!t) t = &automatic;
   if (t->window_bytes != 0 && t->window_bytes != 4096 && t->window_bytes != 8192)
     return set_err(GPD_ERR_INVALID, "gpd_ctx_set_tuning: window_bytes %u (0, 4096 or 8192)", t->window_bytes);
   if (t->shift < -1 || t->shift > 1 || t->reg_prefix < -1 || t->reg_prefix > 1 || t->header_once < -1 ||
-      t->header_once > 1)
-    return set_err(GPD_ERR_INVALID, "gpd_ctx_set_tuning: shift / reg_prefix / header_once outside {-1, 0, 1}");
+      t->header_once > 1 || t->pcap_device_walk < -1 || t->pcap_device_walk > 1)
+    return set_err(GPD_ERR_INVALID,
+                   "gpd_ctx_set_tuning: shift / reg_prefix / header_once / pcap_device_walk outside {-1, 0, 1}");
   if (t->waves_per_simd != 0 && (t->waves_per_simd < 2 || t->waves_per_simd > 4))
     return set_err(GPD_ERR_INVALID, "gpd_ctx_set_tuning: waves_per_simd %d (0, 2, 3 or 4)", t->waves_per_simd);
   ctx->tune = *t;
@@ -500,14 +510,17 @@ static int check_batch(const gpd_batch *in, const gpd_result *out) {
   return GPD_OK;
 }
 
+// n_dev: the packet count is read on the device (at most in->n); geom_n: the packet count the
+// staging choices assume (0: in->n) — both for batches whose records the device walk found.
 static int launch(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, hipStream_t stream,
-                  bool record) {
+                  bool record, const uint32_t *n_dev = nullptr, uint64_t geom_n = 0) {
   gpd::KParams P{};
   P.data = in->data;
   P.data_len = in->data_len;
   P.offset = in->offset;
   P.caplen = in->caplen;
   P.n = in->n;
+  P.n_dev = n_dev;
   P.status = out->status;
   P.layers = out->layers;
   P.net_hash = out->net_hash;
@@ -525,7 +538,8 @@ static int launch(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, hipS
   P.eth_mult = ctx->eth_mult; P.tcp_mult = ctx->tcp_mult; P.udp_mult = ctx->udp_mult;
   P.fixed = ctx->fixed;
   // LDS window per buffer: the smallest of 4/8 KiB that holds a typical 64-packet tile
-  const uint64_t mean_slot = (in->data_len + in->n - 1) / in->n;
+  const uint64_t gn = geom_n ? geom_n : in->n;
+  const uint64_t mean_slot = (in->data_len + gn - 1) / gn;
   P.stage = mean_slot * 64 <= 4096 ? 4096u : 8192u;
   if (ctx->tune.window_bytes) P.stage = ctx->tune.window_bytes;
   P.first = ctx->first;
@@ -648,7 +662,11 @@ static int alloc_slots(gpd_ctx *ctx, uint64_t bytes, uint64_t pkts, bool ext) {
       HIP_TRY(hipHostMalloc(&s.h_ext, pkts * sizeof(gpd_ext_rec), hipHostMallocDefault));
       HIP_TRY(hipMalloc(&s.d_ext, pkts * sizeof(gpd_ext_rec)));
     }
+    HIP_TRY(hipMalloc(&s.d_pw, 5ull * gpd::kPwMaxSeg * 4));
   }
+  HIP_TRY(hipMalloc(&ctx->d_pw_ctl, 2 * sizeof(gpd::PwCtl)));
+  HIP_TRY(hipHostMalloc(&ctx->h_pw_ctl, 2 * sizeof(gpd::PwCtl), hipHostMallocDefault));
+  for (auto &e : ctx->ev_pw) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   ctx->slot_bytes = bytes;
   ctx->slot_pkts = pkts;
   return GPD_OK;
@@ -868,19 +886,14 @@ int gpd_decode_pcap(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, uint64_t max
                             nthreads);
 }
 
-int gpd_decode_pcap_at(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, const gpd_pcap_info *info,
-                       uint64_t pos, uint64_t max_n, const gpd_result *out, uint64_t *n_out,
-                       uint64_t *next_pos, int *stop, int nthreads) {
-  if (!ctx || !buf || !info || !out || !out->status || !out->layers || !n_out)
-    return set_err(GPD_ERR_INVALID, "gpd_decode_pcap: null argument");
-  if (out->ext) return set_err(GPD_ERR_INVALID, "gpd_decode_pcap: ext records not supported");
-  if (pos > len) return set_err(GPD_ERR_INVALID, "gpd_decode_pcap_at: pos beyond the buffer");
-  if (nthreads <= 0) nthreads = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+// The pcap path with the record walk on the host (gpd_pcap.cpp), one part ahead of the chunks.
+static int decode_pcap_host_walk(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, const gpd_pcap_info *info,
+                                 uint64_t pos, uint64_t max_n, const gpd_result *out, uint64_t *n_out,
+                                 uint64_t *next_pos, int *stop, int nthreads) {
   *n_out = 0;
   if (next_pos) *next_pos = pos;
   if (stop) *stop = GPD_PCAP_STOP_LIMIT;
   if (max_n == 0) return GPD_OK;
-  HIP_TRY(hipSetDevice(ctx->device));
   const uint64_t kPkts = 1u << 20, kBytes = 256ull << 20;
   const uint64_t kPart = 1u << 21;  // records per walked part (the first, walked before any
   const uint64_t kPart0 = 1u << 19; // transfer can start, is smaller)
@@ -1021,6 +1034,180 @@ int gpd_decode_pcap_at(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, const gpd
   g_pt_walk = walk_ms;
   g_pt_total = now_ms() - t_call;
   return GPD_OK;
+}
+
+// The pcap path with the record walk on the device (gpd_pcapwalk.hip): the capture travels
+// in fixed chunks of 64 MiB (plus the longest record past them) on two slots, each chunk's
+// records are found in HBM (the walk of chunk k waits for chunk k-1's, which hands it its
+// first record header), decoded there, and their results copied back.  The host reads one
+// 16-byte control block per chunk: how many records it held and whether the device walk
+// stood (status 0).  *handled records were decoded; *resume is the record header where the
+// host walk must take over (a chunk with status 1: a rejected record, a partial record at
+// the end, a speculation the walk missed), UINT64_MAX when the call is complete.
+static int decode_pcap_device_walk(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, const gpd_pcap_info &I,
+                                   uint64_t pos, uint64_t max_n, const gpd_result *out, int nthreads,
+                                   uint64_t *handled, uint64_t *resume, uint64_t *next_pos, int *stop) {
+  constexpr uint64_t kChunk = (uint64_t)gpd::kPwSeg * gpd::kPwMaxSeg;
+  const uint64_t margin = (16ull + I.snaplen + 31ull) & ~15ull;  // the longest record past a chunk
+  const uint64_t cap_pkts = kChunk / GPD_PCAP_RECORD_BYTES;       // records a chunk can hold
+  *handled = 0;
+  *resume = pos;
+  if (I.snaplen > (16u << 20)) return GPD_OK;  // (records that long: the host walk)
+  // the mean record size (the decode's staging choices): the first records, walked here
+  uint64_t mean = 96;
+  {
+    uint64_t sp[64];
+    uint32_t sc[64];
+    gpd::PcapOut o;
+    o.pos64 = sp;
+    o.cap = sc;
+    gpd::PcapResult R;
+    if (gpd::pcap_index_flat(buf, len, I, pos, 64, 1, o, R) != GPD_OK || R.n == 0) return GPD_OK;
+    mean = std::max<uint64_t>(16, (R.next_pos - pos) / R.n);
+  }
+  int rc = alloc_slots(ctx, std::max<uint64_t>(ctx->slot_bytes, kChunk + margin + 64),
+                       std::max<uint64_t>(ctx->slot_pkts, cap_pkts), false);
+  if (rc) return rc;
+  SlotGuard guard{ctx};
+  uint64_t B = pos & ~15ull;  // chunk base (16-byte aligned: the decoder's batch buffer)
+  uint64_t entry = pos - B;   // its first record header
+  uint64_t done = 0;
+  *resume = UINT64_MAX;
+  for (int k = 0;; k++) {
+    auto &s = ctx->slot[k & 1];
+    if (s.busy) {
+      HIP_TRY(hipStreamSynchronize(s.stream));
+      drain_slot(s, out);
+    }
+    const uint64_t own = std::min<uint64_t>(kChunk, len - B);
+    const uint64_t T = std::min<uint64_t>(own + margin, len - B);
+    const bool last = B + own >= len;
+    const uint8_t *src = buf + B;
+    if (!ctx->is_registered(src, T)) {
+      par_memcpy(s.h_data, src, T, nthreads);
+      src = s.h_data;
+    }
+    gpd::PwCtl *dc = ctx->d_pw_ctl + (k & 1), *hc = ctx->h_pw_ctl + (k & 1);
+    HIP_TRY(hipMemcpyAsync(s.d_data, src, T, hipMemcpyHostToDevice, s.stream));
+    if (k == 0) {
+      hc->entry = (uint32_t)entry;
+      HIP_TRY(hipMemcpyAsync(&dc->entry, &hc->entry, 4, hipMemcpyHostToDevice, s.stream));
+    } else {
+      HIP_TRY(hipStreamWaitEvent(s.stream, ctx->ev_pw[(k - 1) & 1], 0));
+    }
+    gpd::PwArgs A{};
+    A.d = s.d_data;
+    A.T = (uint32_t)T;
+    A.own_end = (uint32_t)own;
+    A.nseg = (uint32_t)((own + gpd::kPwSeg - 1) / gpd::kPwSeg);
+    A.snaplen = I.snaplen;
+    A.be = I.big_endian != 0;
+    A.nano = I.nano != 0;
+    A.last = last;
+    A.ctl = dc;
+    A.ctl_next = last ? nullptr : ctx->d_pw_ctl + ((k + 1) & 1);
+    A.st = s.d_pw;
+    A.ex = s.d_pw + gpd::kPwMaxSeg;
+    A.ct = s.d_pw + 2 * gpd::kPwMaxSeg;
+    A.bad = s.d_pw + 3 * gpd::kPwMaxSeg;
+    A.base = s.d_pw + 4 * gpd::kPwMaxSeg;
+    A.off = s.d_off;
+    A.len = s.d_len;
+    hipError_t e = gpd::launch_pcap_walk(A, s.stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(hc, dc, sizeof(gpd::PwCtl), hipMemcpyDeviceToHost, s.stream);
+    if (e == hipSuccess) e = hipEventRecord(ctx->ev_pw[k & 1], s.stream);
+    if (e == hipSuccess) e = gpd::launch_pcap_fill(A, s.stream);
+    if (e != hipSuccess) return set_err(GPD_ERR_HIP, "gpd_decode_pcap: device walk: %s", hipGetErrorString(e));
+    gpd_batch b{s.d_data, T, s.d_off, s.d_len, cap_pkts};
+    gpd_result r{s.d_status, s.d_layers, s.d_nh, s.d_th, s.d_csum, nullptr, out->hdr_off ? s.d_hoff : nullptr};
+    rc = launch(ctx, &b, &r, s.stream, false, &dc->n, std::max<uint64_t>(1, own / mean));
+    if (rc) return rc;
+    HIP_TRY(hipEventSynchronize(ctx->ev_pw[k & 1]));  // this chunk walked: its count
+    const gpd::PwCtl c = *hc;
+    if (c.status != 0) {  // the host walks from this chunk's entry (its decode saw 0 records)
+      HIP_TRY(hipStreamSynchronize(s.stream));
+      *resume = B + entry;
+      break;
+    }
+    const uint64_t take = std::min<uint64_t>(c.n, max_n - done);
+    e = results_d2h(ctx, s, out, done, take);
+    if (e != hipSuccess) return set_err(GPD_ERR_HIP, "gpd_decode_pcap: D2H: %s", hipGetErrorString(e));
+    s.lo = done;
+    s.hi = done + take;
+    s.busy = take > 0;
+    done += take;
+    if (take < c.n) {  // the bound falls inside this chunk: the header of the record after it
+      HIP_TRY(hipMemcpyAsync(s.h_off, s.d_off + take, 4, hipMemcpyDeviceToHost, s.stream));
+      HIP_TRY(hipStreamSynchronize(s.stream));
+      if (next_pos) *next_pos = B + s.h_off[0] - GPD_PCAP_RECORD_BYTES;
+      if (stop) *stop = GPD_PCAP_STOP_LIMIT;
+      break;
+    }
+    if (done == max_n) {
+      if (next_pos) *next_pos = B + c.next;
+      if (stop) *stop = GPD_PCAP_STOP_LIMIT;
+      break;
+    }
+    if (last) {  // status 0 on the last chunk: the walk ended exactly at the capture's end
+      if (next_pos) *next_pos = len;
+      if (stop) *stop = GPD_PCAP_STOP_EOF;
+      break;
+    }
+    entry = c.next - own;
+    B += own;
+  }
+  for (auto &s : ctx->slot) {
+    if (s.busy) {
+      HIP_TRY(hipStreamSynchronize(s.stream));
+      drain_slot(s, out);
+    }
+  }
+  *handled = done;
+  return GPD_OK;
+}
+
+int gpd_decode_pcap_at(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, const gpd_pcap_info *info,
+                       uint64_t pos, uint64_t max_n, const gpd_result *out, uint64_t *n_out,
+                       uint64_t *next_pos, int *stop, int nthreads) {
+  if (!ctx || !buf || !info || !out || !out->status || !out->layers || !n_out)
+    return set_err(GPD_ERR_INVALID, "gpd_decode_pcap: null argument");
+  if (out->ext) return set_err(GPD_ERR_INVALID, "gpd_decode_pcap: ext records not supported");
+  if (out->records) return set_err(GPD_ERR_INVALID, "gpd_decode_pcap: results as SoA arrays only");
+  if (pos > len) return set_err(GPD_ERR_INVALID, "gpd_decode_pcap_at: pos beyond the buffer");
+  if (nthreads <= 0) nthreads = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+  *n_out = 0;
+  if (next_pos) *next_pos = pos;
+  if (stop) *stop = GPD_PCAP_STOP_LIMIT;
+  if (max_n == 0) return GPD_OK;
+  HIP_TRY(hipSetDevice(ctx->device));
+  const double t_call = now_ms();
+  uint64_t done = 0, at = pos;
+  if (ctx->tune.pcap_device_walk != 0) {
+    uint64_t resume;
+    const int rc = decode_pcap_device_walk(ctx, buf, len, *info, pos, max_n, out, nthreads, &done, &resume,
+                                           next_pos, stop);
+    if (rc) return rc;
+    if (resume == UINT64_MAX) {
+      *n_out = done;
+      g_pt_walk = g_pt_walkwait = g_pt_stage = g_pt_sync = g_pt_drain = 0;
+      g_pt_total = now_ms() - t_call;
+      return GPD_OK;
+    }
+    at = resume;
+  }
+  // the host walk from `at` (all of the call, or what the device walk left)
+  gpd_result rest = *out;
+  auto shift = [&](auto *p) { return p ? p + done : p; };
+  rest.status = shift(out->status);
+  rest.layers = shift(out->layers);
+  rest.net_hash = shift(out->net_hash);
+  rest.tp_hash = shift(out->tp_hash);
+  rest.csum = shift(out->csum);
+  rest.hdr_off = shift(out->hdr_off);
+  uint64_t k = 0;
+  const int rc = decode_pcap_host_walk(ctx, buf, len, info, at, max_n - done, &rest, &k, next_pos, stop, nthreads);
+  *n_out = done + k;
+  return rc;
 }
 
 void gpd_decode_pcap_last_times(double *ms6) {
