@@ -1069,28 +1069,29 @@ static int decode_pcap_device_walk(gpd_ctx *ctx, const uint8_t *buf, uint64_t le
                        std::max<uint64_t>(ctx->slot_pkts, cap_pkts), false);
   if (rc) return rc;
   SlotGuard guard{ctx};
-  uint64_t B = pos & ~15ull;  // chunk base (16-byte aligned: the decoder's batch buffer)
-  uint64_t entry = pos - B;   // its first record header
-  uint64_t done = 0;
-  *resume = UINT64_MAX;
-  for (int k = 0;; k++) {
+  // Chunk k's work on slot k & 1: its bytes H2D, then (after chunk k-1's walk) its walk, its
+  // control block back to the host, its fill and its decode.  The next chunk is queued before
+  // the host waits for this one's count, so the copy engine never waits for a walk.
+  auto issue = [&](int k, uint64_t B, uint64_t entry0) -> int {
     auto &s = ctx->slot[k & 1];
     if (s.busy) {
       HIP_TRY(hipStreamSynchronize(s.stream));
       drain_slot(s, out);
+      s.busy = false;
     }
     const uint64_t own = std::min<uint64_t>(kChunk, len - B);
     const uint64_t T = std::min<uint64_t>(own + margin, len - B);
     const bool last = B + own >= len;
     const uint8_t *src = buf + B;
     if (!ctx->is_registered(src, T)) {
+      HIP_TRY(hipStreamSynchronize(s.stream));  // (its staging buffer may still be read)
       par_memcpy(s.h_data, src, T, nthreads);
       src = s.h_data;
     }
     gpd::PwCtl *dc = ctx->d_pw_ctl + (k & 1), *hc = ctx->h_pw_ctl + (k & 1);
     HIP_TRY(hipMemcpyAsync(s.d_data, src, T, hipMemcpyHostToDevice, s.stream));
     if (k == 0) {
-      hc->entry = (uint32_t)entry;
+      hc->entry = (uint32_t)entry0;
       HIP_TRY(hipMemcpyAsync(&dc->entry, &hc->entry, 4, hipMemcpyHostToDevice, s.stream));
     } else {
       HIP_TRY(hipStreamWaitEvent(s.stream, ctx->ev_pw[(k - 1) & 1], 0));
@@ -1120,17 +1121,30 @@ static int decode_pcap_device_walk(gpd_ctx *ctx, const uint8_t *buf, uint64_t le
     if (e != hipSuccess) return set_err(GPD_ERR_HIP, "gpd_decode_pcap: device walk: %s", hipGetErrorString(e));
     gpd_batch b{s.d_data, T, s.d_off, s.d_len, cap_pkts};
     gpd_result r{s.d_status, s.d_layers, s.d_nh, s.d_th, s.d_csum, nullptr, out->hdr_off ? s.d_hoff : nullptr};
-    rc = launch(ctx, &b, &r, s.stream, false, &dc->n, std::max<uint64_t>(1, own / mean));
-    if (rc) return rc;
-    HIP_TRY(hipEventSynchronize(ctx->ev_pw[k & 1]));  // this chunk walked: its count
-    const gpd::PwCtl c = *hc;
+    return launch(ctx, &b, &r, s.stream, false, &dc->n, std::max<uint64_t>(1, own / mean));
+  };
+  uint64_t B = pos & ~15ull;  // chunk base (16-byte aligned: the decoder's batch buffer)
+  uint64_t entry = pos - B;   // its first record header
+  uint64_t done = 0;
+  *resume = UINT64_MAX;
+  rc = issue(0, B, entry);
+  if (rc) return rc;
+  for (int k = 0;; k++) {
+    auto &s = ctx->slot[k & 1];
+    const uint64_t own = std::min<uint64_t>(kChunk, len - B);
+    const bool last = B + own >= len;
+    // queue the next chunk now unless this one should end the call (its records, estimated
+    // from the mean record size, cover what is left)
+    const bool ahead = !last && done + own / mean < max_n;
+    if (ahead && (rc = issue(k + 1, B + own, 0))) return rc;
+    HIP_TRY(hipEventSynchronize(ctx->ev_pw[k & 1]));  // chunk k walked: its count
+    const gpd::PwCtl c = ctx->h_pw_ctl[k & 1];
     if (c.status != 0) {  // the host walks from this chunk's entry (its decode saw 0 records)
-      HIP_TRY(hipStreamSynchronize(s.stream));
       *resume = B + entry;
       break;
     }
     const uint64_t take = std::min<uint64_t>(c.n, max_n - done);
-    e = results_d2h(ctx, s, out, done, take);
+    hipError_t e = results_d2h(ctx, s, out, done, take);
     if (e != hipSuccess) return set_err(GPD_ERR_HIP, "gpd_decode_pcap: D2H: %s", hipGetErrorString(e));
     s.lo = done;
     s.hi = done + take;
@@ -1155,11 +1169,13 @@ static int decode_pcap_device_walk(gpd_ctx *ctx, const uint8_t *buf, uint64_t le
     }
     entry = c.next - own;
     B += own;
+    if (!ahead && (rc = issue(k + 1, B, 0))) return rc;
   }
-  for (auto &s : ctx->slot) {
+  for (auto &s : ctx->slot) {  // (a chunk queued ahead and not needed is waited for and dropped)
+    HIP_TRY(hipStreamSynchronize(s.stream));
     if (s.busy) {
-      HIP_TRY(hipStreamSynchronize(s.stream));
       drain_slot(s, out);
+      s.busy = false;
     }
   }
   *handled = done;
