@@ -88,11 +88,15 @@ int gpd_pcap_index(const uint8_t *buf, uint64_t len, const gpd_pcap_info *info, 
                    uint64_t max_n, uint32_t *offset, uint32_t *caplen, uint32_t *wirelen,
                    uint64_t *ts_ns, uint64_t *n_out, uint64_t *next_pos, int *stop, int nthreads);
 
-/* Index + decode a whole in-memory capture with the context's parser: the records are indexed
- * (as gpd_pcap_index, nthreads as there), then decoded in chunks — the raw bytes of each chunk
- * of records are copied host -> device as they lie in the capture (through pinned staging, or
- * directly when buf lies in memory registered with gpd_host_register), decoded, and the
- * results copied back — with two chunks in flight.  `out` holds host arrays of max_n entries
+/* Index + decode a whole in-memory capture with the context's parser: the raw capture bytes
+ * are copied host -> device in 64 MiB chunks as they lie in the capture (through pinned
+ * staging, or directly when buf lies in memory registered with gpd_host_register), the
+ * records are found in HBM by a parallel walk on the device (gpd_pcapwalk.hip), decoded where
+ * they lie, and the results copied back, with two chunks in flight.  Wherever the device walk
+ * cannot vouch for the records (a record the reference rejects, a capture ending inside a
+ * record, a speculation its stitch refutes), the host walk (as gpd_pcap_index, nthreads as
+ * there) takes over from that chunk, so results, counts, stops and error texts are always the
+ * sequential reader's (gpd_tuning.pcap_device_walk = 0 selects the host walk throughout).  `out` holds host arrays of max_n entries
  * (status and layers required, the rest optional; ext not supported).  Returns like
  * gpd_pcap_index: the records before a rejected one are decoded and counted in *n_out.
  * The record index (about 36 B per record) is kept per calling thread and reused by the
