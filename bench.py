@@ -818,9 +818,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU-baseline timing "
                     "(split over its rows)")
-    ap.add_argument("--host", action="store_true",
+    ap.add_argument("--host", nargs="?", const="plain", default="", choices=("plain", "registered"),
                     help="diagnostic: PCIe-inclusive rate through gpd_decode_host (host arrays in, "
-                    "host arrays out); never the reported metric")
+                    "host arrays out; 'registered': pinned once, as a capture loop would); never "
+                    "the reported metric")
     ap.add_argument("--threads", type=int, default=0, help="host threads for the pcap walker "
                     "(0 = all cores)")
     ap.add_argument("--replay", type=int, default=0, help="pcap64: also replay the capture from "
@@ -955,6 +956,13 @@ def main():
 
     if args.host:  # PCIe-inclusive: repack into pinned slots, H2D, decode, D2H
         res = parser.DecodeBatchHost(batch)
+        regd = []
+        if args.host == "registered":  # a capture loop pins its batch and result arrays once
+            from gopacket_amd._lib import check, lib
+            for a in (batch.data, batch.offset, batch.caplen, res.status, res.layers, res.net_hash,
+                      res.tp_hash, res.csum, res.hdr_off):
+                check(lib.gpd_host_register(parser.ctx().h, a.ctypes.data, a.nbytes), "register")
+                regd.append(a)
         for _ in range(max(1, args.warmup // 2)):
             parser.DecodeBatchHost(batch, out=res)
         steps = max(1, min(args.steps, 5))
@@ -962,13 +970,15 @@ def main():
         for _ in range(steps):
             parser.DecodeBatchHost(batch, out=res)
         el = time.perf_counter() - t0
+        for a in regd:
+            lib.gpd_host_unregister(parser.ctx().h, a.ctypes.data)
         n_err = int(np.count_nonzero((res.status & 3) != 0))
         if rank == 0:
             print(json.dumps({"metric": "DIAGNOSTIC (not the metric): PCIe-inclusive Mpackets/s "
                               "host batch -> gpd_decode_host -> host results",
                               "value": round(n * steps / el / 1e6, 2), "unit": "Mpackets/s",
                               "ms_per_step": round(el / steps * 1e3, 3), "steps": steps,
-                              "config": {"workload": workload, "packets": n,
+                              "config": {"workload": workload, "packets": n, "host_arrays": args.host,
                                          "host_bytes_in": int(batch.data_len) + 8 * n,
                                          "decode_errors_in_batch": n_err},
                               "GBps_in": round((batch.data_len + 8 * n) * steps / el / 1e9, 2)}),
