@@ -764,7 +764,10 @@ int gpd_decode_host(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out) {
       used += in->caplen[j];
       j++;
     }
-    const bool span = j > i && (span_hi - lo16) <= 2 * used + 4096;
+    // (a registered window travels by DMA alone, so it may carry more gap — e.g. an AF_PACKET
+    // ring's frame headers — before a 16-thread host repack of the packets would be cheaper)
+    const bool reg = j > i && ctx->is_registered(in->data + lo16, span_hi - lo16);
+    const bool span = j > i && (span_hi - lo16) <= (reg ? 4 : 2) * used + 4096;
     uint64_t pos = 0;
     if (span) {
       pos = span_hi - lo16;
