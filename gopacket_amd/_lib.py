@@ -36,7 +36,7 @@ class GpdResult(C.Structure):
 class GpdTuning(C.Structure):
     _fields_ = [("window_bytes", C.c_uint32), ("shift", C.c_int32), ("reg_prefix", C.c_int32),
                 ("waves_per_simd", C.c_int32), ("header_once", C.c_int32),
-                ("pcap_device_walk", C.c_int32)]
+                ("device_walk", C.c_int32)]
 
 
 class GpdPcapInfo(C.Structure):
@@ -103,6 +103,7 @@ EXPORTS = {
     "gpd_decode_tpv3": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_int,
                                   C.c_uint64, C.POINTER(GpdResult), C.c_void_p,
                                   C.POINTER(C.c_uint64), C.POINTER(C.c_uint32), C.c_int]),
+    "gpd_decode_tpv3_last_path": (C.c_int, []),
 }
 
 GPD_ERR_PCAP = -5

@@ -25,7 +25,7 @@ ORACLE_LIB = os.path.join(ROOT, "oracle", "libgpd_oracle.so")
 
 SOURCES = [os.path.join(CSRC, "gpd_kernels.hip"), os.path.join(CSRC, "gpd_runtime.cpp"),
            os.path.join(CSRC, "gpd_pcap.cpp"), os.path.join(CSRC, "gpd_flow.hip"),
-           os.path.join(CSRC, "gpd_pcapwalk.hip"),
+           os.path.join(CSRC, "gpd_pcapwalk.hip"), os.path.join(CSRC, "gpd_tpv3walk.hip"),
            os.path.join(CSRC, "gpd_afpacket.cpp")]
 HEADERS = [os.path.join(CSRC, "gpd_internal.h"), os.path.join(ROOT, "include", "gpd.h"),
            os.path.join(ROOT, "include", "gpd_pcap.h"), os.path.join(ROOT, "include", "gpd_flow.h"),

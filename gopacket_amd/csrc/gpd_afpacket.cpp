@@ -127,6 +127,8 @@ int plan_walk(const gpd_tpv3_ring *R, uint32_t first, uint32_t max_blocks, uint6
   return GPD_OK;
 }
 
+thread_local int g_last_path = 0;  // gpd_decode_tpv3_last_path
+
 int run_walk(const gpd_tpv3_ring *R, const std::vector<BlockPlan> &plan, const gpd_tpv3_pkts &pk,
              int nthreads, uint32_t *off32 = nullptr) {
   // nthreads <= 0: the machine's cores, at most 16 (blocks are few and cheap to walk)
@@ -174,6 +176,8 @@ int gpd_tpv3_walk(const gpd_tpv3_ring *ring, uint32_t first_block, uint32_t max_
   return GPD_OK;
 }
 
+int gpd_decode_tpv3_last_path(void) { return g_last_path; }
+
 int gpd_tpv3_release(const gpd_tpv3_ring *ring, uint32_t first_block, uint32_t count) {
   if (!ring || !ring->base || ring->num_blocks == 0)
     return gpd::set_error(GPD_ERR_INVALID, "gpd_tpv3_release: bad ring");
@@ -197,6 +201,35 @@ int gpd_decode_tpv3(gpd_ctx *ctx, const gpd_tpv3_ring *ring, uint32_t first_bloc
   uint64_t n = 0;
   int rc = plan_walk(ring, first_block, max_blocks, max_n, plan, n);
   if (rc || plan.empty()) return rc;
+  {
+    // The walk on the device (gpd_tpv3walk.hip): each block's first emitted packet from its
+    // descriptor here, every other step there.  It declines (tuning, geometry, a walk leaving
+    // its block, a tag to insert) before anything it returned counts; the host path follows.
+    std::vector<gpd::TwPlan> tp(plan.size());
+    for (size_t j = 0; j < plan.size(); j++) {
+      const BlockPlan &bp = plan[j];
+      uint64_t entry = 0;
+      if (bp.emit) {
+        const uint8_t *blk = ring->base + (uint64_t)bp.ring_block * ring->block_size;
+        const tpacket_hdr_v1 &bh = reinterpret_cast<const tpacket_block_desc *>(blk)->hdr.bh1;
+        entry = bh.offset_to_first_pkt;
+        const auto *p0 = reinterpret_cast<const tpacket3_hdr *>(blk + entry);
+        if (p0->tp_len == 0)  // afpacket.go:313-316: the retry's next() (header.go:181-195)
+          entry += p0->tp_next_offset != 0 ? (uint64_t)p0->tp_next_offset
+                                           : tp_align((uint64_t)p0->tp_snaplen + p0->tp_mac);
+      }
+      tp[j] = gpd::TwPlan{bp.ring_block, bp.emit, bp.out, entry};
+    }
+    bool fallback = true;
+    rc = gpd::decode_tpv3_device(ctx, *ring, tp, n, add_vlan_header != 0, pk_out, out, nthreads, &fallback);
+    if (rc) return rc;
+    if (!fallback) {
+      g_last_path = 1;
+      *n_out = n;
+      *blocks_out = (uint32_t)plan.size();
+      return GPD_OK;
+    }
+  }
   // the walk writes straight into the caller's arrays where it has them
   std::vector<uint64_t> off_own;
   std::vector<uint32_t> cap_own, tci_own;
@@ -233,6 +266,7 @@ int gpd_decode_tpv3(gpd_ctx *ctx, const gpd_tpv3_ring *ring, uint32_t first_bloc
     const gpd_batch hb{ring->base, ring_bytes, off32.data(), cap, n};
     rc = gpd_decode_host(ctx, &hb, out);
     if (rc) return rc;
+    g_last_path = 0;
     *n_out = n;
     *blocks_out = (uint32_t)plan.size();
     return GPD_OK;
@@ -309,6 +343,7 @@ int gpd_decode_tpv3(gpd_ctx *ctx, const gpd_tpv3_ring *ring, uint32_t first_bloc
   }
   if (rc) return rc;
   if (e != hipSuccess) return gpd::set_error(GPD_ERR_HIP, "gpd_decode_tpv3: %s", hipGetErrorString(e));
+  g_last_path = 0;
   *n_out = n;
   *blocks_out = (uint32_t)nb;
   return GPD_OK;

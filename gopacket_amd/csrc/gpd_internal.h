@@ -106,6 +106,35 @@ struct PwArgs {
 hipError_t launch_pcap_walk(const PwArgs &A, hipStream_t stream);
 hipError_t launch_pcap_fill(const PwArgs &A, hipStream_t stream);
 
+// The TPACKET_V3 block walk on the GPU (gpd_tpv3walk.hip): one group of consecutive ring
+// blocks in HBM, one workgroup per block.
+constexpr uint32_t kTwWin = 32768;           // LDS window of a block's bytes
+constexpr uint64_t kTwGroup = 64ull << 20;   // bytes of ring blocks per group
+struct TwBlock {      // one walked block (host plan, afpacket.go:303-316 + header.go:144-149)
+  uint32_t entry;     // its first emitted packet header (relative to the block; 16-aligned)
+  uint32_t emit;      // packets the read loop returns from it
+  uint32_t out;       // index of its first packet in the group's output
+  uint32_t pad;
+};
+struct TwArgs {
+  const uint8_t *d;        // the group's blocks, in ring order
+  uint32_t block_size;
+  uint32_t nblk;
+  uint64_t ring_off0;      // the group's first block's offset in the ring
+  const TwBlock *blk;
+  uint32_t *st;            // per block: bit 0 a header or frame outside the block, or a step
+                           // the device walk does not take (0, or not a multiple of 16);
+                           // bit 1 a frame with a nonzero vlan_tci
+  uint32_t *off, *len;     // per packet: frame offset in the group, tp_snaplen
+  uint64_t *ci_off;        // optional capture info (NULL: not written): frame offset in the ring,
+  uint32_t *ci_wire;       //   tp_len,
+  uint64_t *ci_ts;         //   tp_sec * 1e9 + tp_nsec,
+  int32_t *ci_ifx;         //   sockaddr_ll.sll_ifindex,
+  int32_t *ci_vlan;        //   AncillaryVLAN or -1,
+  uint32_t *ci_tci;        //   tp_vlan_tci
+};
+hipError_t launch_tpv3_walk(const TwArgs &A, hipStream_t stream);
+
 // One launch covers at most this many packets, so packet and tile indices are 32-bit.
 constexpr uint64_t kMaxLaunchPackets = 1ull << 30;
 
@@ -153,6 +182,24 @@ int pcap_index_flat(const uint8_t *buf, uint64_t len, const gpd_pcap_info &I, ui
 int pcap_locate(const uint8_t *buf, uint64_t len, const gpd_pcap_info &I, uint64_t pos,
                 const uint64_t *targets, uint64_t k, uint64_t *pos_out, uint64_t *n_total, int *stop,
                 int nthreads);
+}  // namespace gpd
+#include "../../include/gpd_afpacket.h"
+namespace gpd {
+// One user-owned block of a gpd_decode_tpv3 call, as the host planned it (gpd_afpacket.cpp).
+struct TwPlan {
+  uint32_t ring_block;  // index in the ring
+  uint32_t emit;        // packets the read loop returns from it
+  uint64_t out;         // index of its first packet in the call's output
+  uint64_t entry;       // its first emitted packet header (relative to the block)
+};
+// gpd_decode_tpv3 with the block walk on the device (gpd_runtime.cpp): the planned blocks
+// travel to HBM in groups of consecutive ring blocks, are walked there (gpd_tpv3walk.hip)
+// and decoded, and results and capture info come back.  *fallback: the device path does not
+// apply (tuning, geometry, a block the walk rejects, a tagged frame with add_vlan) and the
+// caller runs the host path for the whole call (nothing returned so far counts).
+int decode_tpv3_device(gpd_ctx *ctx, const gpd_tpv3_ring &R, const std::vector<TwPlan> &plan, uint64_t n,
+                       bool add_vlan, const gpd_tpv3_pkts *pk, const gpd_result *out, int nthreads,
+                       bool *fallback);
 
 // Multiplicative hash of a 16-bit key into 2^bits buckets (host and device must agree).
 __host__ __device__ inline uint32_t key_hash(uint32_t key, uint32_t mult, uint32_t bits) {

@@ -235,6 +235,8 @@ struct gpd_ctx {
     uint32_t *h_hoff = nullptr, *d_hoff = nullptr;
     gpd_ext_rec *h_ext = nullptr, *d_ext = nullptr;
     uint32_t *d_pw = nullptr;  // the device pcap walk's per-segment arrays (5 x kPwMaxSeg)
+    uint8_t *d_tw = nullptr, *h_tw = nullptr;  // the device TPACKET_V3 walk's tables + results
+    hipStream_t stream_out = nullptr;          // its D2H (gpd_decode_tpv3)
     uint64_t lo = 0, hi = 0;  // packet range in flight
     bool busy = false;
     bool direct = false;      // its results go straight into the caller's (registered) arrays
@@ -242,6 +244,9 @@ struct gpd_ctx {
   uint64_t slot_bytes = 0, slot_pkts = 0;
   gpd::PwCtl *d_pw_ctl = nullptr, *h_pw_ctl = nullptr;  // one control block per slot
   hipEvent_t ev_pw[2] = {nullptr, nullptr};            // a slot's chunk walked (and its block read back)
+  hipEvent_t ev_tw[4] = {};     // TPACKET_V3 group k & 3's results back
+  hipEvent_t ev_twdec[4] = {};  // ... decoded
+  hipEvent_t ev_twin[2] = {}; // a slot's group bytes H2D done (its staging copy reusable)
   // host ranges pinned with gpd_host_register (H2D reads them in place)
   std::vector<std::pair<const uint8_t *, uint64_t>> registered;
   bool is_registered(const uint8_t *p, uint64_t n) const {
@@ -400,21 +405,29 @@ int gpd_ctx_create(int device, const gpd_config *cfg, gpd_ctx **out) {
 static void free_slots(gpd_ctx *ctx) {
   for (auto &s : ctx->slot) {
     if (s.stream) (void)hipStreamSynchronize(s.stream);
+    if (s.stream_out) (void)hipStreamSynchronize(s.stream_out);
     for (void *p : {(void *)s.h_data, (void *)s.h_off, (void *)s.h_len, (void *)s.h_status,
                     (void *)s.h_csum, (void *)s.h_layers, (void *)s.h_nh, (void *)s.h_th,
-                    (void *)s.h_hoff, (void *)s.h_ext})
+                    (void *)s.h_hoff, (void *)s.h_ext, (void *)s.h_tw})
       if (p) (void)hipHostFree(p);
     for (void *p : {(void *)s.d_data, (void *)s.d_off, (void *)s.d_len, (void *)s.d_status,
                     (void *)s.d_csum, (void *)s.d_layers, (void *)s.d_nh, (void *)s.d_th,
-                    (void *)s.d_hoff, (void *)s.d_ext, (void *)s.d_pw})
+                    (void *)s.d_hoff, (void *)s.d_ext, (void *)s.d_pw, (void *)s.d_tw})
       if (p) (void)hipFree(p);
     if (s.stream) (void)hipStreamDestroy(s.stream);
+    if (s.stream_out) (void)hipStreamDestroy(s.stream_out);
     s = gpd_ctx::Slot{};
   }
   if (ctx->d_pw_ctl) (void)hipFree(ctx->d_pw_ctl);
   if (ctx->h_pw_ctl) (void)hipHostFree(ctx->h_pw_ctl);
   for (auto &e : ctx->ev_pw)
     if (e) (void)hipEventDestroy(e);
+  for (auto &e : ctx->ev_tw)
+    if (e) (void)hipEventDestroy(e), e = nullptr;
+  for (auto &e : ctx->ev_twdec)
+    if (e) (void)hipEventDestroy(e), e = nullptr;
+  for (auto &e : ctx->ev_twin)
+    if (e) (void)hipEventDestroy(e), e = nullptr;
   ctx->d_pw_ctl = ctx->h_pw_ctl = nullptr;
   ctx->ev_pw[0] = ctx->ev_pw[1] = nullptr;
   ctx->slot_bytes = ctx->slot_pkts = 0;
@@ -461,9 +474,9 @@ int gpd_ctx_set_tuning(gpd_ctx *ctx, const gpd_tuning *t) {
   if (t->window_bytes != 0 && t->window_bytes != 4096 && t->window_bytes != 8192)
     return set_err(GPD_ERR_INVALID, "gpd_ctx_set_tuning: window_bytes %u (0, 4096 or 8192)", t->window_bytes);
   if (t->shift < -1 || t->shift > 1 || t->reg_prefix < -1 || t->reg_prefix > 1 || t->header_once < -1 ||
-      t->header_once > 1 || t->pcap_device_walk < -1 || t->pcap_device_walk > 1)
+      t->header_once > 1 || t->device_walk < -1 || t->device_walk > 1)
     return set_err(GPD_ERR_INVALID,
-                   "gpd_ctx_set_tuning: shift / reg_prefix / header_once / pcap_device_walk outside {-1, 0, 1}");
+                   "gpd_ctx_set_tuning: shift / reg_prefix / header_once / device_walk outside {-1, 0, 1}");
   if (t->waves_per_simd != 0 && (t->waves_per_simd < 2 || t->waves_per_simd > 4))
     return set_err(GPD_ERR_INVALID, "gpd_ctx_set_tuning: waves_per_simd %d (0, 2, 3 or 4)", t->waves_per_simd);
   ctx->tune = *t;
@@ -681,6 +694,7 @@ struct SlotGuard {
     for (auto &s : ctx->slot)
       if (s.busy) {
         (void)hipStreamSynchronize(s.stream);
+        if (s.stream_out) (void)hipStreamSynchronize(s.stream_out);
         s.busy = false;
       }
   }
@@ -1047,7 +1061,7 @@ static int decode_pcap_host_walk(gpd_ctx *ctx, const uint8_t *buf, uint64_t len,
 // stood (status 0).  *handled records were decoded; *resume is the record header where the
 // host walk must take over (a chunk with status 1: a rejected record, a partial record at
 // the end, a speculation the walk missed), UINT64_MAX when the call is complete.
-static int decode_pcap_device_walk(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, const gpd_pcap_info &I,
+static int decode_device_walk(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, const gpd_pcap_info &I,
                                    uint64_t pos, uint64_t max_n, const gpd_result *out, int nthreads,
                                    uint64_t *handled, uint64_t *resume, uint64_t *next_pos, int *stop) {
   constexpr uint64_t kChunk = (uint64_t)gpd::kPwSeg * gpd::kPwMaxSeg;
@@ -1201,9 +1215,9 @@ int gpd_decode_pcap_at(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, const gpd
   HIP_TRY(hipSetDevice(ctx->device));
   const double t_call = now_ms();
   uint64_t done = 0, at = pos;
-  if (ctx->tune.pcap_device_walk != 0) {
+  if (ctx->tune.device_walk != 0) {
     uint64_t resume;
-    const int rc = decode_pcap_device_walk(ctx, buf, len, *info, pos, max_n, out, nthreads, &done, &resume,
+    const int rc = decode_device_walk(ctx, buf, len, *info, pos, max_n, out, nthreads, &done, &resume,
                                            next_pos, stop);
     if (rc) return rc;
     if (resume == UINT64_MAX) {
@@ -1240,3 +1254,187 @@ void gpd_decode_pcap_last_times(double *ms6) {
 }
 
 }  // extern "C"
+
+// ---- TPACKET_V3 ring: the blocks H2D in groups, walked and decoded on the device ----
+namespace {
+constexpr uint64_t kTwPkts = 1u << 19;       // packets per group
+constexpr uint64_t kTwMaxBlocks = 16384;     // blocks per group
+constexpr uint64_t kTwTab = kTwMaxBlocks * sizeof(gpd::TwBlock), kTwSt = kTwMaxBlocks * 4;
+// A group's per-packet arrays packed into one region, so one D2H brings them back: decode
+// results, caplen (the walk's, the decode's input), then the capture info, each array
+// 256-byte aligned.  The region is laid out for the group's packet count m.
+enum TwArr { kLayers, kNh, kTh, kStatus, kCsum, kHoff, kCap, kCiOff, kCiTs, kCiWire, kCiIfx, kCiVlan, kCiTci, kTwN };
+constexpr uint64_t kTwW[kTwN] = {8, 8, 8, 4, 4, 4, 4, 8, 8, 4, 4, 4, 4};
+struct TwLay {
+  uint64_t off[kTwN + 1];  // off[kCiOff]: the end of the region without capture info
+  explicit TwLay(uint64_t m) {
+    uint64_t o = 0;
+    for (int a = 0; a < kTwN; a++) {
+      off[a] = o;
+      o += (kTwW[a] * m + 255) & ~255ull;
+    }
+    off[kTwN] = o;
+  }
+};
+const uint64_t kTwRegion = TwLay(kTwPkts).off[kTwN];
+// a slot's d_tw: the group's block table, its status words, its region.  Its h_tw: two of
+// each (a slot holds groups k and k + 2 at once: k + 2 is queued before the host copies k out).
+constexpr uint64_t kTwDevSt = kTwTab;
+inline uint64_t tw_dreg() { return kTwTab + kTwSt; }
+inline uint64_t tw_htab(uint32_t set) { return set * kTwTab; }
+inline uint64_t tw_hst(uint32_t set) { return 2 * kTwTab + set * kTwSt; }
+inline uint64_t tw_hreg(uint32_t set) { return 2 * kTwTab + 2 * kTwSt + set * kTwRegion; }
+}  // namespace
+
+int gpd::decode_tpv3_device(gpd_ctx *ctx, const gpd_tpv3_ring &R, const std::vector<TwPlan> &plan,
+                            uint64_t n, bool add_vlan, const gpd_tpv3_pkts *pk, const gpd_result *out,
+                            int nthreads, bool *fallback) {
+  *fallback = true;
+  const uint64_t B = R.block_size;
+  if (ctx->tune.device_walk == 0 || out->ext || out->records || (B & 15u) || B > kTwGroup || plan.empty())
+    return GPD_OK;
+  for (const auto &p : plan)
+    if (p.emit > kTwPkts || (p.emit && (p.entry + 48 > B || (p.entry & 15u)))) return GPD_OK;
+  if (nthreads <= 0) nthreads = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+  HIP_TRY(hipSetDevice(ctx->device));
+  int rc = alloc_slots(ctx, std::max<uint64_t>(ctx->slot_bytes, kTwGroup),
+                       std::max<uint64_t>(ctx->slot_pkts, kTwPkts), false);
+  if (rc) return rc;
+  for (auto &s : ctx->slot) {
+    if (!s.d_tw) HIP_TRY(hipMalloc(&s.d_tw, tw_dreg() + kTwRegion));
+    if (!s.h_tw) HIP_TRY(hipHostMalloc(&s.h_tw, tw_hreg(2), hipHostMallocDefault));
+    if (!s.stream_out) HIP_TRY(hipStreamCreateWithFlags(&s.stream_out, hipStreamNonBlocking));
+  }
+  for (auto *ev : {ctx->ev_tw, ctx->ev_twdec})
+    for (int q = 0; q < 4; q++)
+      if (!ev[q]) HIP_TRY(hipEventCreateWithFlags(&ev[q], hipEventDisableTiming));
+  for (auto &e : ctx->ev_twin)
+    if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  SlotGuard guard{ctx};
+  const bool ci = pk != nullptr;
+  struct Group {
+    uint64_t lo = 0, m = 0;
+    uint32_t nb = 0, set = 0;
+    bool direct = false;
+  };
+  std::vector<Group> grp;
+  // the caller's array for each region array (NULL: not asked for)
+  void *dst[kTwN] = {out->layers, out->net_hash, out->tp_hash, out->status, out->csum, out->hdr_off,
+                     ci ? pk->caplen : nullptr, ci ? pk->offset : nullptr, ci ? pk->ts_ns : nullptr,
+                     ci ? pk->wire_len : nullptr, ci ? pk->ifindex : nullptr, ci ? pk->vlan : nullptr,
+                     ci ? pk->vlan_tci : nullptr};
+  // group k done: every block walked as the host would, then its results copied out
+  auto complete = [&](size_t k) -> int {
+    HIP_TRY(hipEventSynchronize(ctx->ev_tw[k & 3]));
+    const Group &G = grp[k];
+    const auto &s = ctx->slot[k & 1];
+    const uint32_t *st = reinterpret_cast<const uint32_t *>(s.h_tw + tw_hst(G.set));
+    uint32_t any = 0;
+    for (uint32_t b = 0; b < G.nb; b++) any |= st[b];
+    if ((any & 1u) || (add_vlan && (any & 2u))) return 1;
+    if (!G.direct && G.m) {
+      const TwLay L(G.m);
+      const uint8_t *reg = s.h_tw + tw_hreg(G.set);
+      par_for(G.m, 1u << 15, [&](uint64_t a, uint64_t b) {
+        for (int q = 0; q < kTwN; q++)
+          if (dst[q])
+            std::memcpy(static_cast<uint8_t *>(dst[q]) + (G.lo + a) * kTwW[q], reg + L.off[q] + a * kTwW[q],
+                        (b - a) * kTwW[q]);
+      });
+    }
+    return GPD_OK;
+  };
+  // Group k goes to slot k & 1 and host buffers (k >> 1) & 1.  The slot's stream takes its
+  // bytes, walk and decode; the slot's second stream its D2H, so the next group's bytes do not
+  // queue behind it.  Group k is queued before the host waits for group k - 2 and copies it
+  // out, so neither stream waits for the host.
+  size_t a = 0;
+  while (a < plan.size()) {
+    // the group: consecutive ring blocks (no wrap) within the byte, block and packet bounds
+    size_t b = a + 1;
+    uint64_t m = plan[a].emit;
+    while (b < plan.size() && plan[b].ring_block == plan[b - 1].ring_block + 1 && (b - a + 1) * B <= kTwGroup &&
+           b - a < kTwMaxBlocks && m + plan[b].emit <= kTwPkts)
+      m += plan[b++].emit;
+    const size_t k = grp.size();
+    auto &s = ctx->slot[k & 1];
+    Group G;
+    G.lo = plan[a].out;
+    G.m = m;
+    G.nb = (uint32_t)(b - a);
+    G.set = (uint32_t)((k >> 1) & 1);
+    const uint64_t bytes = (uint64_t)G.nb * B;
+    const TwLay L(std::max<uint64_t>(m, 1));
+    auto *tb = reinterpret_cast<gpd::TwBlock *>(s.h_tw + tw_htab(G.set));  // (group k - 4's: done)
+    for (uint32_t q = 0; q < G.nb; q++)
+      tb[q] = gpd::TwBlock{(uint32_t)plan[a + q].entry, plan[a + q].emit, (uint32_t)(plan[a + q].out - G.lo), 0};
+    const uint8_t *src = R.base + (uint64_t)plan[a].ring_block * B;
+    if (!ctx->is_registered(src, bytes)) {
+      if (k >= 2) HIP_TRY(hipEventSynchronize(ctx->ev_twin[k & 1]));  // group k - 2's bytes are in HBM
+      par_memcpy(s.h_data, src, bytes, nthreads);
+      src = s.h_data;
+    }
+    s.busy = true;  // (work in flight from here: an error exit waits for it)
+    HIP_TRY(hipMemcpyAsync(s.d_data, src, bytes, hipMemcpyHostToDevice, s.stream));
+    HIP_TRY(hipEventRecord(ctx->ev_twin[k & 1], s.stream));
+    HIP_TRY(hipMemcpyAsync(s.d_tw, tb, G.nb * sizeof(gpd::TwBlock), hipMemcpyHostToDevice, s.stream));
+    // the region and status words are group k - 2's until its D2H is done
+    if (k >= 2) HIP_TRY(hipStreamWaitEvent(s.stream, ctx->ev_tw[(k - 2) & 3], 0));
+    uint8_t *dr = s.d_tw + tw_dreg();
+    auto dev = [&](int q) { return dr + L.off[q]; };
+    gpd::TwArgs A{};
+    A.d = s.d_data;
+    A.block_size = (uint32_t)B;
+    A.nblk = G.nb;
+    A.ring_off0 = (uint64_t)plan[a].ring_block * B;
+    A.blk = reinterpret_cast<const gpd::TwBlock *>(s.d_tw);
+    A.st = reinterpret_cast<uint32_t *>(s.d_tw + kTwDevSt);
+    A.off = s.d_off;
+    A.len = reinterpret_cast<uint32_t *>(dev(kCap));
+    if (ci) {
+      A.ci_off = reinterpret_cast<uint64_t *>(dev(kCiOff));
+      A.ci_ts = reinterpret_cast<uint64_t *>(dev(kCiTs));
+      A.ci_wire = reinterpret_cast<uint32_t *>(dev(kCiWire));
+      A.ci_ifx = reinterpret_cast<int32_t *>(dev(kCiIfx));
+      A.ci_vlan = reinterpret_cast<int32_t *>(dev(kCiVlan));
+      A.ci_tci = reinterpret_cast<uint32_t *>(dev(kCiTci));
+    }
+    hipError_t e = gpd::launch_tpv3_walk(A, s.stream);
+    if (e != hipSuccess) return set_err(GPD_ERR_HIP, "gpd_decode_tpv3: device walk: %s", hipGetErrorString(e));
+    if (m) {
+      gpd_batch bt{s.d_data, bytes, s.d_off, A.len, m};
+      gpd_result r{reinterpret_cast<uint32_t *>(dev(kStatus)), reinterpret_cast<uint64_t *>(dev(kLayers)),
+                   reinterpret_cast<uint64_t *>(dev(kNh)), reinterpret_cast<uint64_t *>(dev(kTh)),
+                   reinterpret_cast<uint32_t *>(dev(kCsum)), nullptr,
+                   out->hdr_off ? reinterpret_cast<uint32_t *>(dev(kHoff)) : nullptr};
+      if ((rc = launch(ctx, &bt, &r, s.stream, false))) return rc;
+    }
+    HIP_TRY(hipEventRecord(ctx->ev_twdec[k & 3], s.stream));
+    HIP_TRY(hipStreamWaitEvent(s.stream_out, ctx->ev_twdec[k & 3], 0));
+    HIP_TRY(hipMemcpyAsync(s.h_tw + tw_hst(G.set), A.st, G.nb * 4, hipMemcpyDeviceToHost, s.stream_out));
+    if (m) {
+      G.direct = true;
+      for (int q = 0; q < kTwN; q++)
+        G.direct = G.direct && (!dst[q] || ctx->is_registered(static_cast<uint8_t *>(dst[q]) + G.lo * kTwW[q],
+                                                               m * kTwW[q]));
+      if (G.direct) {
+        for (int q = 0; q < kTwN; q++)
+          if (dst[q])
+            HIP_TRY(hipMemcpyAsync(static_cast<uint8_t *>(dst[q]) + G.lo * kTwW[q], dev(q), m * kTwW[q],
+                                   hipMemcpyDeviceToHost, s.stream_out));
+      } else {
+        HIP_TRY(hipMemcpyAsync(s.h_tw + tw_hreg(G.set), dr, L.off[ci ? kTwN : kCiOff], hipMemcpyDeviceToHost,
+                               s.stream_out));
+      }
+    }
+    HIP_TRY(hipEventRecord(ctx->ev_tw[k & 3], s.stream_out));
+    grp.push_back(G);
+    if (k >= 2 && (rc = complete(k - 2))) return rc == 1 ? GPD_OK : rc;  // (the guard waits)
+    a = b;
+  }
+  for (size_t k = grp.size() >= 2 ? grp.size() - 2 : 0; k < grp.size(); k++)
+    if ((rc = complete(k))) return rc == 1 ? GPD_OK : rc;
+  for (auto &s : ctx->slot) s.busy = false;
+  *fallback = false;
+  return GPD_OK;
+}

@@ -48,7 +48,7 @@ extern "C" {
 
 #define GPD_ABI_VERSION 5  /* 2: ICMPv4 + LLC, 12 objects, 224-B ext; 3: gpd_result.hdr_off;
                               4: gpd_ctx_set_tuning; 5: gpd_tuning.header_once,
-                              gpd_tuning.pcap_device_walk, gpd_result.records */
+                              gpd_tuning.device_walk, gpd_result.records */
 
 /* ---- gopacket LayerType numbers (layertypes.go:14-154, decode.go:105-116) ---- */
 #define GPD_LT_ZERO            0
@@ -344,7 +344,7 @@ typedef struct gpd_tuning {
   int32_t  header_once;   /* 8 KiB windows: decode each 64-packet tile once from headers staged
                              as its windows pass, instead of once per window: -1 automatic
                              (mean slot > 160 B), 0 off, 1 on */
-  int32_t  pcap_device_walk; /* gpd_decode_pcap(_at): find the records in HBM after the raw
+  int32_t  device_walk; /* gpd_decode_pcap(_at): find the records in HBM after the raw
                                bytes arrive (gpd_pcapwalk.hip) instead of walking them on the
                                host first: -1 automatic (on), 0 off, 1 on */
 } gpd_tuning;

@@ -21,9 +21,11 @@
  *                     getVLAN/next (header.go:151-195), CaptureInfo (afpacket.go:318-326)
  *   gpd_tpv3_release  releaseCurrentPacket -> v3wrapper.clearStatus (afpacket.go:282-287,
  *                     header.go:162-164) for the walked blocks
- *   gpd_decode_tpv3   that loop feeding DecodingLayerParser.DecodeLayers: walk + H2D of the
- *                     walked blocks + gpd_decode + D2H; OptAddVLANHeader's tag insertion
- *                     (header.go:74-82, 168-173) for the packets it applies to
+ *   gpd_decode_tpv3   that loop feeding DecodingLayerParser.DecodeLayers: H2D of the walked
+ *                     blocks + the walk on the device (gpd_tuning.device_walk, the default;
+ *                     or on the host) + gpd_decode + D2H of results and capture info;
+ *                     OptAddVLANHeader's tag insertion (header.go:74-82, 168-173) for the
+ *                     packets it applies to (the host path)
  *
  * Ring layout (linux/if_packet.h; TPACKET_V3): block k starts at ring + k * block_size with a
  * struct tpacket_block_desc; its tpacket_hdr_v1 gives block_status, num_pkts and
@@ -74,6 +76,9 @@ int gpd_decode_tpv3(gpd_ctx *ctx, const gpd_tpv3_ring *ring, uint32_t first_bloc
                     uint32_t max_blocks, int add_vlan_header, uint64_t max_n,
                     const gpd_result *out, const gpd_tpv3_pkts *pk, uint64_t *n_out,
                     uint32_t *blocks_out, int nthreads);
+/* Which walk the calling thread's last successful gpd_decode_tpv3 used: 1 the device walk
+ * (gpd_tuning.device_walk; the blocks walked in HBM), 0 the host walk (diagnostic). */
+int gpd_decode_tpv3_last_path(void);
 
 #ifdef __cplusplus
 }

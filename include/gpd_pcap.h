@@ -96,7 +96,7 @@ int gpd_pcap_index(const uint8_t *buf, uint64_t len, const gpd_pcap_info *info, 
  * cannot vouch for the records (a record the reference rejects, a capture ending inside a
  * record, a speculation its stitch refutes), the host walk (as gpd_pcap_index, nthreads as
  * there) takes over from that chunk, so results, counts, stops and error texts are always the
- * sequential reader's (gpd_tuning.pcap_device_walk = 0 selects the host walk throughout).
+ * sequential reader's (gpd_tuning.device_walk = 0 selects the host walk throughout).
  * `out` holds host arrays of max_n entries (status and layers required, the rest optional;
  * ext and records not supported).  Returns like gpd_pcap_index: the records before a
  * rejected one are decoded and counted in *n_out.  The host walk's record index (12 B per

@@ -186,3 +186,90 @@ def test_decode_tpv3_matches_oracle(add_vlan):
     if add_vlan:  # tagged frames decode with the inserted Dot1Q layer
         tagged = [j for j, r in enumerate(ref_pk) if len(r["data"]) == r["snaplen"] + 4]
         assert tagged and all(res.decoded(j)[:2] == [L.LayerTypeEthernet, L.LayerTypeDot1Q] for j in tagged[:50])
+
+
+def _decode_both(arr, bs, nb, first, register=False, **kw):
+    """DecodeTPv3 with the walk on the device and on the host: equal results, capture info,
+    block counts and errors.  Returns (path of the device-walk call, packets, blocks)."""
+    from gopacket_amd import _lib, afpacket as A
+    from gopacket_amd import parser as P
+    got = []
+    for dw in (1, 0):
+        parser = P.NewDecodingLayerParser(L.LayerTypeEthernet, *[P.DECODER_BY_NAME[k]() for k in P.DECODER_BY_NAME])
+        parser.Tuning = {"device_walk": dw}
+        ring = A.TPv3Ring(arr, bs, nb)
+        ring.offset = first
+        if register:
+            _lib.check(_lib.lib.gpd_host_register(parser.ctx().h, arr.ctypes.data, arr.nbytes), "register")
+        try:
+            res, ci, nblk = parser.DecodeTPv3(ring, **kw)
+            got.append((res, ci, nblk, None, _lib.lib.gpd_decode_tpv3_last_path()))
+        except _lib.GpdError as e:
+            got.append((None, None, None, str(e), None))
+        finally:
+            if register:
+                _lib.lib.gpd_host_unregister(parser.ctx().h, arr.ctypes.data)
+    (r1, c1, b1, e1, path), (r0, c0, b0, e0, _) = got
+    assert e1 == e0
+    if e1 is not None:
+        return None, 0, 0
+    assert b1 == b0 and len(r1) == len(r0)
+    for f in ("status", "layers", "net_hash", "tp_hash", "csum", "hdr_off"):
+        assert np.array_equal(getattr(r1, f), getattr(r0, f)), f
+    for f in ("offset", "caplen", "length", "ts_ns", "ifindex", "vlan", "vlan_tci"):
+        assert np.array_equal(getattr(c1, f), getattr(c0, f)), f
+    return path, len(r1), b1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("first", [0, 61])
+def test_device_walk_equals_host_walk(first):
+    """The block walk in HBM (gpd_tpv3walk.hip) returns what the host walk does: wrap-around,
+    empty and kernel-owned blocks, both tp_next_offset forms, VLAN flags and tags, bounds."""
+    pk = _packets(3000)
+    rng = np.random.default_rng(first)
+    vlan = [(int(rng.integers(1, 1 << 16)), bool(rng.integers(0, 2))) if rng.random() < 0.3 else (0, False)
+            for _ in pk]
+    arr, used = synth.make_tpv3_ring(pk, 1 << 16, 64, first_block=first, vlan=vlan, empty_blocks=(2, 5),
+                                     kernel_blocks=(9,), wire_extra=3)
+    path, n, nblk = _decode_both(arr, 1 << 16, 64, first)
+    assert path == 1 and 0 < n < len(pk) and nblk == 9  # walk position 9 is still the kernel's
+    for kw in ({"max_blocks": 7}, {"max_n": 1000}, {"add_vlan_header": True}):
+        path, n, nblk = _decode_both(arr, 1 << 16, 64, first, **kw)
+        # frames carrying a tag with OptAddVLANHeader: the host path inserts it
+        assert path == (0 if "add_vlan_header" in kw else 1)
+    arr2, _ = synth.make_tpv3_ring(pk, 1 << 16, 64, first_block=first)  # no tags at all
+    assert _decode_both(arr2, 1 << 16, 64, first, add_vlan_header=True)[0] == 1
+
+
+@pytest.mark.gpu
+def test_device_walk_quirks_and_corrupt_blocks():
+    pk = _packets(600)
+    bs = 1 << 13
+    arr, used = synth.make_tpv3_ring(pk, bs, 64)
+    first = int(np.frombuffer(arr[16:20].tobytes(), np.uint32)[0])
+    q = arr.copy()
+    q[first + 16:first + 20] = 0                  # block 0, packet 0: tp_len = 0 (skipped)
+    q[used[1] * bs + 12:used[1] * bs + 16] = 0    # block 1: num_pkts = 0 (one stale packet)
+    path, n, _ = _decode_both(q, bs, 64, 0)
+    assert path == 1 and n == len(pk) - 1 - (int(np.frombuffer(arr[used[1] * bs + 12:used[1] * bs + 16].tobytes(),
+                                                                 np.uint32)[0]) - 1)
+    # a tp_next_offset that leaves the block, one that is not 4-byte aligned, a frame past
+    # the block's end: the device walk declines and the host walk reports (or returns) the same
+    b3 = used[3] * bs + first
+    for off, val in ((b3, bs), (b3, 100 * 16 + 2), (b3 + 12, bs)):
+        c = arr.copy()
+        c[off:off + 4] = np.frombuffer(np.uint32(val).tobytes(), np.uint8)
+        _decode_both(c, bs, 64, 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("register", [False, True])
+def test_device_walk_several_groups(register):
+    """A 256 x 1 MiB ring of IMIX frames (several 64 MiB groups in flight on both slots),
+    the ring registered or not."""
+    b = synth.make_imix(400000, seed=0x77)
+    pk = [b.packet(i) for i in range(b.n)]
+    arr, used = synth.make_tpv3_ring(pk, 1 << 20, 256)
+    path, n, nblk = _decode_both(arr, 1 << 20, 256, 0, register=register, max_n=1 << 19)
+    assert path == 1 and n == len(pk) and nblk == len(used) and nblk * (1 << 20) > 2 * (64 << 20)

@@ -1,4 +1,4 @@
-"""The pcap record walk on the device (gpd_pcapwalk.hip, gpd_tuning.pcap_device_walk): every
+"""The pcap record walk on the device (gpd_pcapwalk.hip, gpd_tuning.device_walk): every
 gpd_decode_pcap(_at) result — records, their decoded words, the record count, where the walk
 stops and why, the error text — equals the host walk's (gpd_pcap.cpp, itself pinned to
 pcapgo's ReadPacketData loop by tests/test_pcap*.py), over captures that span several 64 MiB
@@ -26,7 +26,7 @@ def _parser(device_walk):
     p = P.NewDecodingLayerParser(L.LayerTypeEthernet, P.Ethernet(), P.Dot1Q(), P.IPv4(), P.IPv6(),
                                  P.IPv6ExtensionSkipper(), P.TCP(), P.UDP(), P.VXLAN(), P.Payload(),
                                  P.Fragment())
-    p.Tuning = {"pcap_device_walk": device_walk}
+    p.Tuning = {"device_walk": device_walk}
     return p
 
 
