@@ -244,6 +244,7 @@ struct gpd_ctx {
   uint64_t slot_bytes = 0, slot_pkts = 0;
   gpd::PwCtl *d_pw_ctl = nullptr, *h_pw_ctl = nullptr;  // one control block per slot
   hipEvent_t ev_pw[2] = {nullptr, nullptr};            // a slot's chunk walked (and its block read back)
+  hipStream_t tw_in = nullptr;  // TPACKET_V3 groups' bytes H2D, one after another
   hipEvent_t ev_tw[4] = {};     // TPACKET_V3 group k & 3's results back
   hipEvent_t ev_twdec[4] = {};  // ... decoded
   hipEvent_t ev_twin[2] = {}; // a slot's group bytes H2D done (its staging copy reusable)
@@ -403,6 +404,7 @@ int gpd_ctx_create(int device, const gpd_config *cfg, gpd_ctx **out) {
 }
 
 static void free_slots(gpd_ctx *ctx) {
+  if (ctx->tw_in) (void)hipStreamSynchronize(ctx->tw_in);
   for (auto &s : ctx->slot) {
     if (s.stream) (void)hipStreamSynchronize(s.stream);
     if (s.stream_out) (void)hipStreamSynchronize(s.stream_out);
@@ -422,6 +424,8 @@ static void free_slots(gpd_ctx *ctx) {
   if (ctx->h_pw_ctl) (void)hipHostFree(ctx->h_pw_ctl);
   for (auto &e : ctx->ev_pw)
     if (e) (void)hipEventDestroy(e);
+  if (ctx->tw_in) (void)hipStreamDestroy(ctx->tw_in);
+  ctx->tw_in = nullptr;
   for (auto &e : ctx->ev_tw)
     if (e) (void)hipEventDestroy(e), e = nullptr;
   for (auto &e : ctx->ev_twdec)
@@ -693,6 +697,7 @@ struct SlotGuard {
   ~SlotGuard() {
     for (auto &s : ctx->slot)
       if (s.busy) {
+        if (ctx->tw_in) (void)hipStreamSynchronize(ctx->tw_in);
         (void)hipStreamSynchronize(s.stream);
         if (s.stream_out) (void)hipStreamSynchronize(s.stream_out);
         s.busy = false;
@@ -1305,6 +1310,7 @@ int gpd::decode_tpv3_device(gpd_ctx *ctx, const gpd_tpv3_ring &R, const std::vec
     if (!s.h_tw) HIP_TRY(hipHostMalloc(&s.h_tw, tw_hreg(2), hipHostMallocDefault));
     if (!s.stream_out) HIP_TRY(hipStreamCreateWithFlags(&s.stream_out, hipStreamNonBlocking));
   }
+  if (!ctx->tw_in) HIP_TRY(hipStreamCreateWithFlags(&ctx->tw_in, hipStreamNonBlocking));
   for (auto *ev : {ctx->ev_tw, ctx->ev_twdec})
     for (int q = 0; q < 4; q++)
       if (!ev[q]) HIP_TRY(hipEventCreateWithFlags(&ev[q], hipEventDisableTiming));
@@ -1344,10 +1350,10 @@ int gpd::decode_tpv3_device(gpd_ctx *ctx, const gpd_tpv3_ring &R, const std::vec
     }
     return GPD_OK;
   };
-  // Group k goes to slot k & 1 and host buffers (k >> 1) & 1.  The slot's stream takes its
-  // bytes, walk and decode; the slot's second stream its D2H, so the next group's bytes do not
-  // queue behind it.  Group k is queued before the host waits for group k - 2 and copies it
-  // out, so neither stream waits for the host.
+  // Group k goes to slot k & 1 and host buffers (k >> 1) & 1.  Its bytes go on the copy
+  // stream (all groups in order), its walk and decode on the slot's stream, its D2H on the
+  // slot's second stream, so no transfer queues behind a kernel.  Group k is queued before the
+  // host waits for group k - 2 and copies it out, so no stream waits for the host.
   size_t a = 0;
   while (a < plan.size()) {
     // the group: consecutive ring blocks (no wrap) within the byte, block and packet bounds
@@ -1375,8 +1381,12 @@ int gpd::decode_tpv3_device(gpd_ctx *ctx, const gpd_tpv3_ring &R, const std::vec
       src = s.h_data;
     }
     s.busy = true;  // (work in flight from here: an error exit waits for it)
-    HIP_TRY(hipMemcpyAsync(s.d_data, src, bytes, hipMemcpyHostToDevice, s.stream));
-    HIP_TRY(hipEventRecord(ctx->ev_twin[k & 1], s.stream));
+    // the bytes on the copy stream, right behind the previous group's (the link stays busy
+    // while groups are walked), once group k - 2's decode has read the slot's buffer
+    if (k >= 2) HIP_TRY(hipStreamWaitEvent(ctx->tw_in, ctx->ev_twdec[(k - 2) & 3], 0));
+    HIP_TRY(hipMemcpyAsync(s.d_data, src, bytes, hipMemcpyHostToDevice, ctx->tw_in));
+    HIP_TRY(hipEventRecord(ctx->ev_twin[k & 1], ctx->tw_in));
+    HIP_TRY(hipStreamWaitEvent(s.stream, ctx->ev_twin[k & 1], 0));
     HIP_TRY(hipMemcpyAsync(s.d_tw, tb, G.nb * sizeof(gpd::TwBlock), hipMemcpyHostToDevice, s.stream));
     // the region and status words are group k - 2's until its D2H is done
     if (k >= 2) HIP_TRY(hipStreamWaitEvent(s.stream, ctx->ev_tw[(k - 2) & 3], 0));
