@@ -91,6 +91,7 @@ EXPORTS = {
                                   C.POINTER(C.c_uint64), C.c_void_p]),
     "gpd_flow_destroy": (C.c_int, [C.c_void_p]),
     "gpd_flow_test_fingerprint_bits": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "gpd_flow_test_counter_bits": (C.c_int, [C.c_void_p, C.c_uint32]),
     "gpd_flow_keys": (C.c_int, [C.c_void_p, C.POINTER(GpdBatch), C.POINTER(GpdResult), C.c_uint32,
                                 C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p]),
     "gpd_flow_insert_keys": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]),

@@ -41,6 +41,13 @@ enum : uint32_t { FS_FLOWS = 0, FS_PACKETS, FS_NOKEY, FS_FULL, FS_COLL, FS_EXPOR
 
 static_assert(sizeof(gpd_flow_key) == 64, "gpd_flow_key layout (include/gpd_flow.h)");
 
+// A record's counters inside the table (gpd_flow_export unpacks them into the public
+// gpd_flow_rec fields): `bytes` holds one packed word, packets << B | bytes mod 2^B (B =
+// kCountBits), so one 64-bit atomicAdd updates both; `packets` holds the spills, (carries
+// out of the byte field) << 32 + (wraps of the 64-bit word), each in units of 2^B bytes and
+// 2^(64-B) packets.  See add_run.
+constexpr uint32_t kCountBits = 40;
+
 struct FlowParams {
   const uint8_t *data;
   uint64_t data_len;
@@ -60,6 +67,7 @@ struct FlowParams {
   // the key the verify would compare against); one word per wave iteration
   uint64_t *made = nullptr;
   uint64_t fp_mask = ~0ull;  // gpd_flow_test_fingerprint_bits (all ones in production)
+  uint32_t cbits = kCountBits;  // gpd_flow_test_counter_bits (kCountBits in production)
 };
 
 // The key of packet i as 10 words: src[16], dst[16], ports (raw wire bytes), types.  Returns
@@ -155,21 +163,44 @@ __device__ __forceinline__ bool fold_run(bool counted, uint64_t s, uint64_t &mn,
 // its totals plainly; every other run adds them with atomics in the verify launch, after
 // those stores (the launch boundary orders them).  So a new flow costs its claim CAS and
 // plain stores, and the atomics are left to packets of flows that already existed.
-__device__ __forceinline__ void store_run(gpd_flow_rec &r, uint64_t mn, uint64_t mx, uint64_t pb) {
+__device__ __forceinline__ void store_run(gpd_flow_rec &r, uint64_t mn, uint64_t mx, uint64_t pb, uint32_t B) {
+  const uint64_t pk = pb >> kPktShift, by = pb & ((1ull << kPktShift) - 1ull);
   r.first = mn;
   r.last = mx;
-  r.packets = pb >> kPktShift;
-  r.bytes = pb & ((1ull << kPktShift) - 1ull);
+  r.bytes = (pk << B) | (by & ((1ull << B) - 1ull));  // (pk <= 64 < 2^(64-B))
+  r.packets = (by >> B) << 32;
 }
-__device__ __forceinline__ void add_run(gpd_flow_rec &r, uint64_t mn, uint64_t mx, uint64_t pb) {
+// The packed add.  x = pk << B + by goes in with one atomicAdd that returns the old word; the
+// lane whose add carried out of the byte field (c carries: ((old mod 2^B) + by) >> B) takes
+// c << B back out of the packet field and books c carries, and the lane whose add or
+// take-back wrapped the 64-bit word books +1 / -1 wraps.  Each carry and wrap is seen by
+// exactly the lane that caused it, so at the end of the launch
+//   packets = (word >> B) + wraps << (64-B),   bytes = (word mod 2^B) + carries << B
+// exactly, in any order of the adds.  Carries need 2^40 bytes and wraps 2^24 packets of one
+// flow in production, so the spill atomics are rare; the add's return is the price.
+__device__ __forceinline__ void add_run(gpd_flow_rec &r, uint64_t mn, uint64_t mx, uint64_t pb, uint32_t B) {
   // `first` only falls: a read at or below mn (a flow seen in an earlier batch) proves the
   // min a no-op; a stale read is only ever larger, and then the atomic runs
   const uint64_t f = *reinterpret_cast<volatile uint64_t *>(&r.first);
   if (mn < f) atomicMin(reinterpret_cast<unsigned long long *>(&r.first), (unsigned long long)mn);
   atomicMax(reinterpret_cast<unsigned long long *>(&r.last), (unsigned long long)mx);
-  atomicAdd(reinterpret_cast<unsigned long long *>(&r.packets), (unsigned long long)(pb >> kPktShift));
-  atomicAdd(reinterpret_cast<unsigned long long *>(&r.bytes),
-            (unsigned long long)(pb & ((1ull << kPktShift) - 1ull)));
+  const uint64_t pk = pb >> kPktShift, by = pb & ((1ull << kPktShift) - 1ull), M = (1ull << B) - 1ull;
+  const uint64_t x = (pk << B) + by;
+  auto *w = reinterpret_cast<unsigned long long *>(&r.bytes);
+  const uint64_t old = atomicAdd(w, (unsigned long long)x);
+  const uint64_t c = ((old & M) + by) >> B;
+  uint64_t spill = (c << 32) + (old + x < old ? 1ull : 0ull);
+  if (c) {
+    const uint64_t back = c << B;
+    const uint64_t old2 = atomicAdd(w, (unsigned long long)(0ull - back));
+    if (old2 < back) spill -= 1ull;
+  }
+  if (spill) atomicAdd(reinterpret_cast<unsigned long long *>(&r.packets), (unsigned long long)spill);
+}
+__host__ __device__ inline void unpack_counts(gpd_flow_rec &r, uint32_t B) {
+  const uint64_t w = r.bytes, sp = r.packets;
+  r.packets = (w >> B) + ((sp & 0xFFFFFFFFull) << (64u - B));
+  r.bytes = (w & ((1ull << B) - 1ull)) + ((sp >> 32) << B);
 }
 
 // Sequence number and captured length of item i.
@@ -263,7 +294,7 @@ __global__ __launch_bounds__(kFlowThreads) void flow_insert_kernel(FlowParams P)
     uint64_t mn = seq, mx = seq, pb = (1ull << kPktShift) | caplen;
     uint32_t start;
     const bool tail = fold_run(counted, s, mn, mx, pb, start);
-    if (counted && tail && ((made >> start) & 1ull)) store_run(P.tab[s], mn, mx, pb);
+    if (counted && tail && ((made >> start) & 1ull)) store_run(P.tab[s], mn, mx, pb, P.cbits);
     if (live) P.flow_id[i] = !keyed ? GPD_FLOW_NONE : full ? GPD_FLOW_FULL : (uint32_t)s;
     wave_tally(t_flows, created);
     wave_tally(t_packets, counted);
@@ -297,7 +328,7 @@ __global__ __launch_bounds__(kFlowThreads) void flow_verify_kernel(FlowParams P)
       pb = (1ull << kPktShift) | caplen;
     }
     const bool tail = fold_run(counted, id, mn, mx, pb, start);
-    if (counted && tail && !((made >> start) & 1ull)) add_run(P.tab[id], mn, mx, pb);
+    if (counted && tail && !((made >> start) & 1ull)) add_run(P.tab[id], mn, mx, pb, P.cbits);
     if (i < P.n) {
       uint32_t k[10];
       uint64_t seq;
@@ -461,13 +492,15 @@ __global__ __launch_bounds__(kFlowThreads) void flow_reset_kernel(gpd_flow_rec *
 __global__ __launch_bounds__(kFlowThreads) void flow_export_kernel(const gpd_flow_rec *tab, uint64_t cap,
                                                                   gpd_flow_rec *out, uint32_t *idx,
                                                                   uint64_t max,
-                                                                  unsigned long long *stats) {
+                                                                  unsigned long long *stats, uint32_t B) {
   for (uint64_t s = blockIdx.x * (uint64_t)kFlowThreads + threadIdx.x; s < cap;
        s += (uint64_t)gridDim.x * kFlowThreads) {
     if (tab[s].fp != 0) {
       const unsigned long long j = atomicAdd(stats + FS_EXPORT, 1ull);
       if (j < max) {
-        out[j] = tab[s];
+        gpd_flow_rec r = tab[s];
+        unpack_counts(r, B);
+        out[j] = r;
         idx[j] = (uint32_t)s;
       }
     }
@@ -487,6 +520,7 @@ struct gpd_flowtable {
   uint64_t *made = nullptr;  // insert -> verify claim bits, one word per 64 packets, grown on use
   uint64_t made_words = 0;
   uint64_t fp_mask = ~0ull;  // gpd_flow_test_fingerprint_bits
+  uint32_t cbits = gpd::kCountBits;  // gpd_flow_test_counter_bits
 };
 
 #define FLOW_TRY(expr)                                                                      \
@@ -574,6 +608,7 @@ int gpd_flow_insert(gpd_flowtable *ft, const gpd_batch *in, const gpd_result *re
   FLOW_TRY(grow_made(ft, in->n));
   P.made = ft->made;
   P.fp_mask = ft->fp_mask;
+  P.cbits = ft->cbits;
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid(grid_for(in->n, ft->num_cus)), block(gpd::kFlowThreads);
   hipLaunchKernelGGL(gpd::flow_insert_kernel<false>, grid, block, 0, s, P);
@@ -655,6 +690,7 @@ int gpd_flow_insert_keys(gpd_flowtable *ft, const gpd_flow_key *keys, uint64_t n
   FLOW_TRY(grow_made(ft, n));
   P.made = ft->made;
   P.fp_mask = ft->fp_mask;  // (key records carry their sender's fingerprint; recomputed here)
+  P.cbits = ft->cbits;
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid(grid_for(n, ft->num_cus)), block(gpd::kFlowThreads);
   hipLaunchKernelGGL(gpd::flow_insert_kernel<true>, grid, block, 0, s, P);
@@ -697,7 +733,7 @@ int gpd_flow_export(gpd_flowtable *ft, gpd_flow_rec *out, uint32_t *rec_index, u
   if (e == hipSuccess) e = hipMemsetAsync(ft->stats + gpd::FS_EXPORT, 0, sizeof(unsigned long long), s);
   if (e == hipSuccess) {
     hipLaunchKernelGGL(gpd::flow_export_kernel, dim3(grid_for(ft->cap, ft->num_cus)),
-                       dim3(gpd::kFlowThreads), 0, s, ft->tab, ft->cap, d_out, d_idx, m, ft->stats);
+                       dim3(gpd::kFlowThreads), 0, s, ft->tab, ft->cap, d_out, d_idx, m, ft->stats, ft->cbits);
     e = hipGetLastError();
   }
   std::vector<gpd_flow_rec> recs(m);
@@ -725,6 +761,13 @@ int gpd_flow_test_fingerprint_bits(gpd_flowtable *ft, uint32_t bits) {
   if (!ft || bits == 0 || bits > 64)
     return gpd::set_error(GPD_ERR_INVALID, "gpd_flow_test_fingerprint_bits: bits %u outside [1, 64]", bits);
   ft->fp_mask = bits == 64 ? ~0ull : (1ull << bits) - 1ull;
+  return GPD_OK;
+}
+
+int gpd_flow_test_counter_bits(gpd_flowtable *ft, uint32_t bits) {
+  if (!ft || bits == 0 || bits > 57)
+    return gpd::set_error(GPD_ERR_INVALID, "gpd_flow_test_counter_bits: bits %u outside [1, 57]", bits);
+  ft->cbits = bits;
   return GPD_OK;
 }
 

@@ -76,6 +76,11 @@ class FlowTable:
         `bits` bits so that distinct keys collide; call on an empty table."""
         check(lib.gpd_flow_test_fingerprint_bits(self.h, int(bits)), "gpd_flow_test_fingerprint_bits")
 
+    def _test_counter_bits(self, bits: int) -> None:
+        """Testing hook (gpd_flow_test_counter_bits): split the packed counter word at `bits`
+        so that its fields carry and wrap within a test; call on an empty table."""
+        check(lib.gpd_flow_test_counter_bits(self.h, int(bits)), "gpd_flow_test_counter_bits")
+
     def Stats(self, stream=None) -> dict:
         st = FlowStats()
         check(lib.gpd_flow_stats_get(self.h, C.byref(st), self._stream(stream)), "gpd_flow_stats_get")

@@ -96,6 +96,10 @@ int gpd_flow_destroy(gpd_flowtable *ft);
  * collision path (GPD_FLOW_COLLISION, gpd_flow_stats.collisions) runs.  Call it on an empty
  * table (after create or reset); a production table never calls it. */
 int gpd_flow_test_fingerprint_bits(gpd_flowtable *ft, uint32_t bits);
+/* Testing hook: split each record's packed counter word at `bits` (1..57; 40 = the default)
+ * instead, so that its byte field carries and its packet field wraps within a test's
+ * packets and the exact spill accounting runs.  Call it on an empty table. */
+int gpd_flow_test_counter_bits(gpd_flowtable *ft, uint32_t bits);
 
 /* ---- flow-affine sharding over several GPUs ----
  * The reference's fan-out idiom sends every packet of a flow to one worker picked by the

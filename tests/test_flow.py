@@ -327,3 +327,33 @@ def test_flow_fingerprint_collisions_are_flagged(bits):
         assert int(r["packets"]) == len(on)
         assert int(r["bytes"]) == int(batch.caplen[on].astype(np.int64).sum())
         assert (int(r["first"]), int(r["last"])) == (int(on.min()), int(on.max()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits", [1, 7, 12, 57])
+def test_flow_counter_spills_are_exact(bits):
+    """The packed counter word (packets << B | bytes mod 2^B, one atomicAdd) split at a test
+    width (gpd_flow_test_counter_bits): with B = 1..12 nearly every add carries out of the
+    byte field, with B = 57 the 7-bit packet field wraps after 128 packets of a flow.  Hot
+    flows (~70 packets each per batch) and bursts, accumulated over four batches, so new-flow
+    stores, existing-flow adds, carries, wraps and take-back borrows all run; every exported
+    record must equal the oracle's group-by."""
+    import torch
+    from gopacket_amd import flows as FL
+    from gopacket_amd import parser as P
+    parts = [_hot_batch(20000, 300, 11), _burst_batch(20000, 200, 12), _hot_batch(20000, 300, 11),
+             _burst_batch(20000, 200, 12)]
+    parser = P.NewDecodingLayerParser(L.LayerTypeEthernet, *[P.DECODER_BY_NAME[k]() for k in P.DECODER_BY_NAME])
+    ft = FL.NewFlowTable(parser, 1 << 14)
+    ft._test_counter_bits(bits)
+    ids, base = [], 0
+    for batch in parts:
+        db, dr = _decode_dev(parser, batch)
+        ids.append(ft.Insert(db, dr, index_base=base).cpu().numpy().view(np.uint32))
+        base += batch.n
+    torch.cuda.synchronize()
+    allp = PacketBatch.from_packets([b.packet(i) for b in parts for i in range(b.n)])
+    ref = O.decode(allp, L.LayerTypeEthernet, parser.decoders, 0, ext=False, nthreads=8)
+    flows_ref, per_ref = F.group(allp, ref)
+    assert max(f["packets"] for f in flows_ref.values()) > 128
+    _check_table(allp, None, np.concatenate(ids), ft, flows_ref, per_ref)
