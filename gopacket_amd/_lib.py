@@ -105,6 +105,9 @@ EXPORTS = {
                                   C.c_uint64, C.POINTER(GpdResult), C.c_void_p,
                                   C.POINTER(C.c_uint64), C.POINTER(C.c_uint32), C.c_int]),
     "gpd_decode_tpv3_last_path": (C.c_int, []),
+    # include/gpd_defrag.h
+    "gpd_ip4_fragments": (C.c_int, [C.c_void_p, C.POINTER(GpdBatch), C.POINTER(GpdResult), C.c_void_p,
+                                    C.c_uint64, C.POINTER(C.c_uint64), C.c_void_p]),
 }
 
 GPD_ERR_PCAP = -5

@@ -135,6 +135,21 @@ struct TwArgs {
 };
 hipError_t launch_tpv3_walk(const TwArgs &A, hipStream_t stream);
 
+// The IPv4 fragment hand-off (include/gpd_defrag.h): the decoded batch and tables in P (its
+// status/layers or rec, and hdr_off, are the decode's results), scratch and the records.
+}  // namespace gpd
+#include "../../include/gpd_defrag.h"
+namespace gpd {
+struct FragArgs {
+  KParams P;
+  gpd_ip4_frag *out;
+  uint32_t max_out;   // records written: min(candidates, max_out)
+  uint32_t nblk;      // ceil(n / 256)
+  uint32_t *blk;      // nblk + 1: per-block candidate counts -> exclusive prefix; [nblk] = total
+  uint32_t *idx;      // n: the candidates' packet indices in order
+};
+hipError_t launch_ip4_frag(const FragArgs &A, hipStream_t stream, int num_cus);
+
 // One launch covers at most this many packets, so packet and tile indices are 32-bit.
 constexpr uint64_t kMaxLaunchPackets = 1ull << 30;
 

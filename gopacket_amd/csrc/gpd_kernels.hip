@@ -1971,6 +1971,153 @@ static hipError_t launch_s(const KParams &P, hipStream_t stream, int num_cus) {
   return launch_t<8192, false, EXT, PAGES, true, 4>(P, stream, num_cus);
 }
 
+// ---------------------------------------------------------------- IPv4 fragment hand-off
+// include/gpd_defrag.h: the packets for which IPv4Defragmenter.DefragIPv4 does not return the
+// layer unchanged (dontDefrag, ip4defrag/defrag.go:162-172), in packet order, with the key and
+// securityChecks verdict (:175-198).  Four launches: per-256-packet candidate counts, their
+// exclusive scan, the candidates' packet indices in order, and one record per candidate.
+
+// Can packet i's IPv4 object (the last IPv4 in decoded) be a fragment?  From the result words
+// first: a fragmented IPv4 layer ends the decode (ip4.go:281-286, its next layer is
+// gopacket.Fragment, which decodes nothing further), so decoded ends [.., IPv4, Fragment], or
+// [.., IPv4] with Fragment unregistered (stop type 3) or the payload empty (stop 0).  Then the
+// flags/offset word of the header (ip4.go:193,200-201), which also rules out DF (:164-166).
+__device__ __forceinline__ bool frag_candidate(const KParams &P, uint32_t i) {
+  uint32_t st;
+  uint64_t lw;
+  if (P.rec) {
+    st = P.rec[i].status;
+    lw = P.rec[i].layers;
+  } else {
+    st = P.status[i];
+    lw = P.layers[i];
+  }
+  if (GPD_STATUS_NET_EPT(st) != 1u) return false;  // the last network layer is not IPv4
+  const uint32_t nl = GPD_STATUS_NLAYERS(st);
+  if (nl <= GPD_CORE_MAX_LAYERS && !GPD_STATUS_SATURATED(st)) {
+    const uint32_t last = GPD_LAYERS_CODE(lw, nl - 1), stop = GPD_LAYERS_STOP(lw);
+    const bool maybe = (last == GPD_C_FRAGMENT && nl >= 2 && GPD_LAYERS_CODE(lw, nl - 2) == GPD_C_IPV4) ||
+                       (last == GPD_C_IPV4 && (stop == 0 || stop == GPD_LT_FRAGMENT));
+    if (!maybe) return false;
+  }
+  const uint32_t net = GPD_HDR_NET(P.hdr_off[i]);
+  if (net == GPD_HDR_NONE) return true;  // header past byte 65534: the record pass decides
+  const uint32_t dlen = (uint32_t)P.data_len;
+  const uint32_t off = min(P.offset[i], dlen);
+  const uint8_t *h = P.data + off + net;  // a decoded IPv4 header: 20 bytes inside the packet
+  const uint32_t flags = h[6] >> 5, fo = ((h[6] & 0x1Fu) << 8) | h[7];
+  if (flags & 2u) return false;  // IPv4DontFragment
+  return (flags & 1u) || fo != 0;
+}
+
+__global__ __launch_bounds__(256) void frag_count_kernel(FragArgs A) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  const int c = __syncthreads_count(i < A.P.n && frag_candidate(A.P, i));
+  if (threadIdx.x == 0) A.blk[blockIdx.x] = (uint32_t)c;
+}
+
+// One workgroup: exclusive scan of the per-block counts in place; blk[nblk] = the total.
+__global__ __launch_bounds__(1024) void frag_scan_kernel(FragArgs A) {
+  __shared__ uint32_t part[1024];
+  const uint32_t t = threadIdx.x, per = (A.nblk + 1023u) / 1024u;
+  const uint32_t lo = min(t * per, A.nblk), hi = min(lo + per, A.nblk);
+  uint32_t s = 0;
+  for (uint32_t k = lo; k < hi; ++k) s += A.blk[k];
+  part[t] = s;
+  __syncthreads();
+  for (uint32_t d = 1; d < 1024u; d <<= 1) {
+    const uint32_t v = t >= d ? part[t - d] : 0u;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[t] - s;
+  for (uint32_t k = lo; k < hi; ++k) {
+    const uint32_t c = A.blk[k];
+    A.blk[k] = run;
+    run += c;
+  }
+  if (t == 1023u) A.blk[A.nblk] = part[1023];
+}
+
+__global__ __launch_bounds__(256) void frag_index_kernel(FragArgs A) {
+  __shared__ uint32_t wsum[4];
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x, lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  const bool c = i < A.P.n && frag_candidate(A.P, i);
+  const uint64_t m = __ballot(c);
+  if (lane == 0) wsum[w] = (uint32_t)__popcll(m);
+  __syncthreads();
+  if (c) {
+    uint32_t r = A.blk[blockIdx.x];
+    for (uint32_t k = 0; k < w; ++k) r += wsum[k];
+    A.idx[r + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = i;
+  }
+}
+
+// One lane per candidate: the generic decoder re-runs the packet for the IPv4 object's exact
+// state (its Contents/Payload, so a TSO Length of 0 and truncation come out as the reference
+// leaves them), then dontDefrag and securityChecks on it.
+template <bool PAGES>
+__global__ __launch_bounds__(256) void frag_record_kernel(FragArgs A) {
+  const KParams &P = A.P;
+  const uint32_t cnt = min(A.blk[A.nblk], A.max_out);
+  if (cnt <= blockIdx.x * 256u) return;
+  for (uint32_t k = threadIdx.x; k < P.image_words; k += 256) reinterpret_cast<uint32_t *>(g_lds)[k] = P.image[k];
+  __syncthreads();
+  const Tab<PAGES> T{P.pages,    P.eth_base, P.tcp_base, P.udp_base, P.eth_bits,
+                     P.tcp_bits, P.udp_bits, P.eth_mult, P.tcp_mult, P.udp_mult};
+  const uint32_t dlen = (uint32_t)P.data_len;
+  const uint32_t options = P.options & ~kDiagMask;
+  for (uint32_t j = blockIdx.x * 256u + threadIdx.x; j < cnt; j += gridDim.x * 256u) {
+    const uint32_t i = A.idx[j];
+    const uint32_t off = min(P.offset[i], dlen), len = min(P.caplen[i], dlen - off);
+    gpd_ext_rec e;
+    decode_packet<true>(GlbSrc{P.data, off}, len, T, P.first, options, &e);
+    const gpd_layer_rec o = e.obj[GPD_OBJ_IPV4];
+    gpd_ip4_frag r{};
+    r.packet = i;
+    r.verdict = GPD_FRAG_WHOLE;
+    if (e.obj_valid & (1u << GPD_OBJ_IPV4)) {
+      const uint8_t *h = P.data + off + o.contents_off;
+      const uint32_t raw_len = ((uint32_t)h[2] << 8) | h[3], ff = ((uint32_t)h[6] << 8) | h[7];
+      r.net_off = o.contents_off;
+      for (int b = 0; b < 4; ++b) {
+        r.src[b] = h[12 + b];
+        r.dst[b] = h[16 + b];
+      }
+      r.id = (uint16_t)(((uint32_t)h[4] << 8) | h[5]);
+      r.flags = (uint8_t)(ff >> 13);
+      r.frag_offset = (uint16_t)(ff & 0x1FFFu);
+      r.ihl = h[0] & 0x0Fu;
+      // ip4.go:214-218: Length 0 => len(data); the decode then keeps all of data, so it is
+      // Contents + Payload
+      r.length = (uint16_t)(raw_len ? raw_len : o.contents_len + o.payload_len);
+      r.payload_len = o.payload_len;
+      const bool dont = (r.flags & 2u) || (!(r.flags & 1u) && r.frag_offset == 0);  // defrag.go:162-172
+      const uint16_t frag_size = (uint16_t)(r.length - (uint16_t)(r.ihl * 4u));        // :176
+      if (dont) r.verdict = GPD_FRAG_WHOLE;
+      else if (frag_size < 8u) r.verdict = GPD_FRAG_TOO_SMALL;                           // :179
+      else if (r.frag_offset > 8183u) r.verdict = GPD_FRAG_OFFSET;                       // :185
+      else if ((uint16_t)(r.frag_offset * 8u + r.length) > 65535u) r.verdict = GPD_FRAG_OVERRUN;  // :192, uint16
+      else r.verdict = GPD_FRAG_INSERT;
+    }
+    A.out[j] = r;
+  }
+}
+
+hipError_t launch_ip4_frag(const FragArgs &A, hipStream_t stream, int num_cus) {
+  if (A.nblk == 0) return hipSuccess;
+  hipLaunchKernelGGL(frag_count_kernel, dim3(A.nblk), dim3(256), 0, stream, A);
+  hipLaunchKernelGGL(frag_scan_kernel, dim3(1), dim3(1024), 0, stream, A);
+  hipLaunchKernelGGL(frag_index_kernel, dim3(A.nblk), dim3(256), 0, stream, A);
+  if (A.max_out == 0) return hipGetLastError();
+  const size_t lds = (A.P.image_words * 4u + 15u) & ~15u;
+  const unsigned grid = (unsigned)std::min<uint64_t>((uint64_t)num_cus * 2, (A.max_out + 255u) / 256u);
+  if (A.P.use_pages) hipLaunchKernelGGL(frag_record_kernel<true>, dim3(grid), dim3(256), lds, stream, A);
+  else hipLaunchKernelGGL(frag_record_kernel<false>, dim3(grid), dim3(256), lds, stream, A);
+  return hipGetLastError();
+}
+
 bool fast_eligible(const KParams &P) {
   // the fast kernel: Ethernet first and registered, hashed tables, no extended records
   return !P.ext && !P.use_pages && P.fixed && P.first == GPD_LT_ETHERNET &&

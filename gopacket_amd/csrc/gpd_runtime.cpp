@@ -650,6 +650,58 @@ int gpd_sync(gpd_ctx *ctx, void *stream) {
   return GPD_OK;
 }
 
+// ---- IPv4 fragment hand-off (include/gpd_defrag.h) ----
+int gpd_ip4_fragments(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *res, gpd_ip4_frag *out,
+                      uint64_t max_out, uint64_t *count, void *stream) {
+  if (!ctx || !in || !res || !count) return set_err(GPD_ERR_INVALID, "gpd_ip4_fragments: null argument");
+  *count = 0;
+  if (in->n == 0) return GPD_OK;
+  if (in->n > 0xFFFFFF00ull) return set_err(GPD_ERR_INVALID, "gpd_ip4_fragments: batch of %llu packets (max 2^32 - 256)",
+                                            (unsigned long long)in->n);
+  if (!in->data || !in->offset || !in->caplen)
+    return set_err(GPD_ERR_INVALID, "gpd_ip4_fragments: batch data/offset/caplen must be non-NULL");
+  if (!res->hdr_off || (!res->records && (!res->status || !res->layers)))
+    return set_err(GPD_ERR_INVALID, "gpd_ip4_fragments: needs hdr_off and status + layers (or records)");
+  if (max_out && !out) return set_err(GPD_ERR_INVALID, "gpd_ip4_fragments: null out with max_out > 0");
+  HIP_TRY(hipSetDevice(ctx->device));
+  gpd::FragArgs A{};
+  gpd::KParams &P = A.P;
+  P.data = in->data;
+  P.data_len = in->data_len;
+  P.offset = in->offset;
+  P.caplen = in->caplen;
+  P.n = in->n;
+  P.status = res->status;
+  P.layers = res->layers;
+  P.rec = res->records;
+  P.hdr_off = res->hdr_off;
+  P.image = ctx->d_image;
+  P.pages = ctx->d_pages;
+  P.image_words = ctx->image_words;
+  P.use_pages = ctx->use_pages;
+  P.eth_base = ctx->eth_base; P.tcp_base = ctx->tcp_base; P.udp_base = ctx->udp_base;
+  P.eth_bits = ctx->eth_bits; P.tcp_bits = ctx->tcp_bits; P.udp_bits = ctx->udp_bits;
+  P.eth_mult = ctx->eth_mult; P.tcp_mult = ctx->tcp_mult; P.udp_mult = ctx->udp_mult;
+  P.fixed = ctx->fixed;
+  P.first = ctx->first;
+  P.decoders = ctx->decoders;
+  P.options = ctx->options;
+  A.out = out;
+  A.max_out = (uint32_t)std::min<uint64_t>(max_out, in->n);
+  A.nblk = (uint32_t)((in->n + 255) / 256);
+  A.blk = static_cast<uint32_t *>(gpd::ctx_scratch(ctx, 12, ((size_t)A.nblk + 1) * 4));
+  A.idx = static_cast<uint32_t *>(gpd::ctx_scratch(ctx, 13, (size_t)in->n * 4));
+  if (!A.blk || !A.idx) return set_err(GPD_ERR_NOMEM, "gpd_ip4_fragments: scratch allocation failed");
+  const hipStream_t s = (hipStream_t)stream;
+  hipError_t e = gpd::launch_ip4_frag(A, s, ctx->num_cus);
+  if (e != hipSuccess) return set_err(GPD_ERR_HIP, "gpd_ip4_fragments launch: %s", hipGetErrorString(e));
+  uint32_t total = 0;
+  HIP_TRY(hipMemcpyAsync(&total, A.blk + A.nblk, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  *count = total;
+  return GPD_OK;
+}
+
 // ---- host-memory path: chunked, double-buffered pinned H2D -> decode -> D2H ----
 static int alloc_slots(gpd_ctx *ctx, uint64_t bytes, uint64_t pkts, bool ext) {
   if (ctx->slot_bytes >= bytes && ctx->slot_pkts >= pkts && (!ext || ctx->slot[0].d_ext))
