@@ -47,6 +47,13 @@ static_assert(sizeof(gpd_flow_key) == 64, "gpd_flow_key layout (include/gpd_flow
 // out of the byte field) << 32 + (wraps of the 64-bit word), each in units of 2^B bytes and
 // 2^(64-B) packets.  See add_run.
 constexpr uint32_t kCountBits = 40;
+// A record's fingerprint word: the key's 56-bit fingerprint, and in the top byte the epoch
+// (1..255, the insert launch's number mod 255) of the launch that claimed it.  The claim's CAS
+// writes both, so every lane that finds the record reads the epoch with the fingerprint: a
+// record claimed by an earlier launch has its key and counters published (the launch
+// boundary), and the insert updates and checks it at once; one claimed in this launch (or
+// 255 launches ago: deferring is always correct) is left to the verify launch.
+constexpr uint64_t kFpBits = (1ull << 56) - 1ull;
 
 struct FlowParams {
   const uint8_t *data;
@@ -66,8 +73,9 @@ struct FlowParams {
   // insert -> verify: bit l of word w set when packet 64w+l claimed its record (and so wrote
   // the key the verify would compare against); one word per wave iteration
   uint64_t *made = nullptr;
-  uint64_t fp_mask = ~0ull;  // gpd_flow_test_fingerprint_bits (all ones in production)
+  uint64_t fp_mask = kFpBits;  // gpd_flow_test_fingerprint_bits (kFpBits in production)
   uint32_t cbits = kCountBits;  // gpd_flow_test_counter_bits (kCountBits in production)
+  uint64_t tag = 1ull << 56;    // this launch's epoch (1..255) in the fingerprint word's top byte
 };
 
 // The key of packet i as 10 words: src[16], dst[16], ports (raw wire bytes), types.  Returns
@@ -203,6 +211,15 @@ __host__ __device__ inline void unpack_counts(gpd_flow_rec &r, uint32_t B) {
   r.bytes = (w & ((1ull << B) - 1ull)) + ((sp >> 32) << B);
 }
 
+// Is the record's stored key the packet's key?
+__device__ __forceinline__ bool same_key(const gpd_flow_rec &r, const uint32_t (&k)[10]) {
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(r.src);
+  bool same = k[9] == ((uint32_t)r.net_type | ((uint32_t)r.tp_type << 8) | ((uint32_t)r.addr_len << 16));
+#pragma unroll
+  for (int j = 0; j < 9; j++) same = same && w[j] == k[j];
+  return same;
+}
+
 // Sequence number and captured length of item i.
 template <bool KEYS>
 __device__ __forceinline__ void item_seq(const FlowParams &P, uint64_t i, uint64_t &seq,
@@ -236,7 +253,7 @@ __device__ __forceinline__ bool item_key(const FlowParams &P, uint64_t i, uint32
 
 template <bool KEYS>
 __global__ __launch_bounds__(kFlowThreads) void flow_insert_kernel(FlowParams P) {
-  unsigned long long t_flows = 0, t_packets = 0, t_nokey = 0, t_full = 0;
+  unsigned long long t_flows = 0, t_packets = 0, t_nokey = 0, t_full = 0, t_coll = 0;
   for (uint64_t i = blockIdx.x * (uint64_t)kFlowThreads + threadIdx.x; i - threadIdx.x < P.n;
        i += (uint64_t)gridDim.x * kFlowThreads) {
     const bool live = i < P.n;
@@ -244,7 +261,7 @@ __global__ __launch_bounds__(kFlowThreads) void flow_insert_kernel(FlowParams P)
     uint64_t seq = 0;
     uint32_t caplen = 0;
     const bool keyed = live && item_key<KEYS>(P, i, k, seq, caplen);
-    bool created = false, full = false;
+    bool created = false, full = false, pre = false;
     uint64_t s = 0;
     // A lane whose left neighbour holds the same fingerprint (a burst) follows the same
     // probe sequence to the same record: only the first lane of each such run probes, and
@@ -262,7 +279,8 @@ __global__ __launch_bounds__(kFlowThreads) void flow_insert_kernel(FlowParams P)
         // a fingerprint is final; only an empty slot needs the compare-and-swap
         unsigned long long old = *reinterpret_cast<volatile unsigned long long *>(&P.tab[s].fp);
         if (old == 0ull)
-          old = atomicCAS(reinterpret_cast<unsigned long long *>(&P.tab[s].fp), 0ull, (unsigned long long)fp);
+          old = atomicCAS(reinterpret_cast<unsigned long long *>(&P.tab[s].fp), 0ull,
+                          (unsigned long long)(fp | P.tag));
         if (old == 0ull) {  // claimed: store the key (read by the verify launch)
           gpd_flow_rec &r = P.tab[s];
           uint32_t *w = reinterpret_cast<uint32_t *>(r.src);
@@ -274,7 +292,10 @@ __global__ __launch_bounds__(kFlowThreads) void flow_insert_kernel(FlowParams P)
           created = true;
           break;
         }
-        if (old == fp) break;
+        if ((old & kFpBits) == fp) {
+          pre = (old & ~kFpBits) != P.tag;  // claimed by an earlier launch
+          break;
+        }
         s = (s + 1) & P.mask;
       }
       if (probe > P.mask) full = true;
@@ -282,20 +303,31 @@ __global__ __launch_bounds__(kFlowThreads) void flow_insert_kernel(FlowParams P)
     if (lead != ~0ull) {  // run members take the slot their run's first lane found
       const uint32_t start = 63u - (uint32_t)__builtin_clzll(lead & ((2ull << lane) - 1ull));
       const uint64_t hs = __shfl(s, (int)start, 64);
-      const bool hfull = __shfl((int)full, (int)start, 64) != 0;
+      const int hflags = __shfl((int)full | ((int)pre << 1), (int)start, 64);
       if (keyed && !probes) {
         s = hs;
-        full = hfull;
+        full = (hflags & 1) != 0;
+        pre = (hflags & 2) != 0;
       }
     }
     const uint64_t made = __ballot(created);
-    if (lane == 0u && i < P.n) P.made[i >> 6] = made;  // i = the wave's first packet
+    // done: the packet's update and key check happen here (its record is its own, or was
+    // published before this launch); the verify launch skips these packets
+    const uint64_t done = __ballot(created || (pre && keyed && !full));
+    if (lane == 0u && i < P.n) P.made[i >> 6] = done;  // i = the wave's first packet
     const bool counted = keyed && !full;
     uint64_t mn = seq, mx = seq, pb = (1ull << kPktShift) | caplen;
     uint32_t start;
     const bool tail = fold_run(counted, s, mn, mx, pb, start);
-    if (counted && tail && ((made >> start) & 1ull)) store_run(P.tab[s], mn, mx, pb, P.cbits);
-    if (live) P.flow_id[i] = !keyed ? GPD_FLOW_NONE : full ? GPD_FLOW_FULL : (uint32_t)s;
+    if (counted && tail) {
+      if ((made >> start) & 1ull) store_run(P.tab[s], mn, mx, pb, P.cbits);
+      else if (pre) add_run(P.tab[s], mn, mx, pb, P.cbits);
+    }
+    bool bad = false;
+    if (counted && pre) bad = !same_key(P.tab[s], k);
+    if (bad) P.flow_id[i] = (uint32_t)s | GPD_FLOW_COLLISION;
+    if (live && !bad) P.flow_id[i] = !keyed ? GPD_FLOW_NONE : full ? GPD_FLOW_FULL : (uint32_t)s;
+    wave_tally(t_coll, bad);
     wave_tally(t_flows, created);
     wave_tally(t_packets, counted);
     wave_tally(t_nokey, live && !keyed);
@@ -305,6 +337,7 @@ __global__ __launch_bounds__(kFlowThreads) void flow_insert_kernel(FlowParams P)
   wave_flush(P.stats + FS_PACKETS, t_packets);
   wave_flush(P.stats + FS_NOKEY, t_nokey);
   wave_flush(P.stats + FS_FULL, t_full);
+  wave_flush(P.stats + FS_COLL, t_coll);
 }
 
 // Second pass: the counter updates of runs that found an existing record, and every item's
@@ -335,12 +368,7 @@ __global__ __launch_bounds__(kFlowThreads) void flow_verify_kernel(FlowParams P)
       // a packet that claimed its record wrote that record's key itself
       const bool mine = (made >> (threadIdx.x & 63u)) & 1ull;
       if (counted && !mine && item_key<KEYS>(P, i, k, seq, caplen)) {
-        const gpd_flow_rec &r = P.tab[id];
-        const uint32_t *w = reinterpret_cast<const uint32_t *>(r.src);
-        bool same = k[9] == ((uint32_t)r.net_type | ((uint32_t)r.tp_type << 8) | ((uint32_t)r.addr_len << 16));
-#pragma unroll
-        for (int j = 0; j < 9; j++) same = same && w[j] == k[j];
-        if (!same) {
+        if (!same_key(P.tab[id], k)) {
           P.flow_id[i] = id | GPD_FLOW_COLLISION;
           bad = true;
         }
@@ -499,6 +527,7 @@ __global__ __launch_bounds__(kFlowThreads) void flow_export_kernel(const gpd_flo
       const unsigned long long j = atomicAdd(stats + FS_EXPORT, 1ull);
       if (j < max) {
         gpd_flow_rec r = tab[s];
+        r.fp &= kFpBits;  // the fingerprint without its epoch
         unpack_counts(r, B);
         out[j] = r;
         idx[j] = (uint32_t)s;
@@ -519,9 +548,16 @@ struct gpd_flowtable {
   uint64_t parts_words = 0;
   uint64_t *made = nullptr;  // insert -> verify claim bits, one word per 64 packets, grown on use
   uint64_t made_words = 0;
-  uint64_t fp_mask = ~0ull;  // gpd_flow_test_fingerprint_bits
+  uint64_t fp_mask = gpd::kFpBits;  // gpd_flow_test_fingerprint_bits
   uint32_t cbits = gpd::kCountBits;  // gpd_flow_test_counter_bits
+  uint32_t epoch = 0;                 // insert launches so far, mod 255
 };
+
+// The next insert launch's epoch tag (1..255 in the fingerprint word's top byte).
+static uint64_t next_tag(gpd_flowtable *ft) {
+  ft->epoch = ft->epoch % 255u + 1u;
+  return (uint64_t)ft->epoch << 56;
+}
 
 #define FLOW_TRY(expr)                                                                      \
   do {                                                                                     \
@@ -609,6 +645,7 @@ int gpd_flow_insert(gpd_flowtable *ft, const gpd_batch *in, const gpd_result *re
   P.made = ft->made;
   P.fp_mask = ft->fp_mask;
   P.cbits = ft->cbits;
+  P.tag = next_tag(ft);
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid(grid_for(in->n, ft->num_cus)), block(gpd::kFlowThreads);
   hipLaunchKernelGGL(gpd::flow_insert_kernel<false>, grid, block, 0, s, P);
@@ -691,6 +728,7 @@ int gpd_flow_insert_keys(gpd_flowtable *ft, const gpd_flow_key *keys, uint64_t n
   P.made = ft->made;
   P.fp_mask = ft->fp_mask;  // (key records carry their sender's fingerprint; recomputed here)
   P.cbits = ft->cbits;
+  P.tag = next_tag(ft);
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid(grid_for(n, ft->num_cus)), block(gpd::kFlowThreads);
   hipLaunchKernelGGL(gpd::flow_insert_kernel<true>, grid, block, 0, s, P);
@@ -760,7 +798,7 @@ int gpd_flow_export(gpd_flowtable *ft, gpd_flow_rec *out, uint32_t *rec_index, u
 int gpd_flow_test_fingerprint_bits(gpd_flowtable *ft, uint32_t bits) {
   if (!ft || bits == 0 || bits > 64)
     return gpd::set_error(GPD_ERR_INVALID, "gpd_flow_test_fingerprint_bits: bits %u outside [1, 64]", bits);
-  ft->fp_mask = bits == 64 ? ~0ull : (1ull << bits) - 1ull;
+  ft->fp_mask = bits >= 56 ? gpd::kFpBits : (1ull << bits) - 1ull;
   return GPD_OK;
 }
 

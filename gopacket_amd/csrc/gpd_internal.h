@@ -144,8 +144,9 @@ struct FragArgs {
   KParams P;
   gpd_ip4_frag *out;
   uint32_t max_out;   // records written: min(candidates, max_out)
-  uint32_t nblk;      // ceil(n / 256)
+  uint32_t nblk;      // ceil(n / 2048)
   uint32_t *blk;      // nblk + 1: per-block candidate counts -> exclusive prefix; [nblk] = total
+  uint64_t *mask;     // ceil(n / 64): bit l of word w = packet 64w + l is a candidate
   uint32_t *idx;      // n: the candidates' packet indices in order
 };
 hipError_t launch_ip4_frag(const FragArgs &A, hipStream_t stream, int num_cus);

@@ -1974,8 +1974,9 @@ static hipError_t launch_s(const KParams &P, hipStream_t stream, int num_cus) {
 // ---------------------------------------------------------------- IPv4 fragment hand-off
 // include/gpd_defrag.h: the packets for which IPv4Defragmenter.DefragIPv4 does not return the
 // layer unchanged (dontDefrag, ip4defrag/defrag.go:162-172), in packet order, with the key and
-// securityChecks verdict (:175-198).  Four launches: per-256-packet candidate counts, their
-// exclusive scan, the candidates' packet indices in order, and one record per candidate.
+// securityChecks verdict (:175-198).  Four launches: per-2048-packet candidate counts (and one
+// candidate bit per packet), their exclusive scan, the candidates' packet indices in order, and
+// one record per candidate.
 
 // Can packet i's IPv4 object (the last IPv4 in decoded) be a fragment?  From the result words
 // first: a fragmented IPv4 layer ends the decode (ip4.go:281-286, its next layer is
@@ -2010,48 +2011,71 @@ __device__ __forceinline__ bool frag_candidate(const KParams &P, uint32_t i) {
   return (flags & 1u) || fo != 0;
 }
 
+// Packets per counting workgroup: 8 rounds of 256 lanes; bit l of mask word w is packet 64w + l.
+constexpr uint32_t kFragBlock = 2048;
+
 __global__ __launch_bounds__(256) void frag_count_kernel(FragArgs A) {
-  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-  const int c = __syncthreads_count(i < A.P.n && frag_candidate(A.P, i));
-  if (threadIdx.x == 0) A.blk[blockIdx.x] = (uint32_t)c;
-}
-
-// One workgroup: exclusive scan of the per-block counts in place; blk[nblk] = the total.
-__global__ __launch_bounds__(1024) void frag_scan_kernel(FragArgs A) {
-  __shared__ uint32_t part[1024];
-  const uint32_t t = threadIdx.x, per = (A.nblk + 1023u) / 1024u;
-  const uint32_t lo = min(t * per, A.nblk), hi = min(lo + per, A.nblk);
-  uint32_t s = 0;
-  for (uint32_t k = lo; k < hi; ++k) s += A.blk[k];
-  part[t] = s;
-  __syncthreads();
-  for (uint32_t d = 1; d < 1024u; d <<= 1) {
-    const uint32_t v = t >= d ? part[t - d] : 0u;
-    __syncthreads();
-    part[t] += v;
-    __syncthreads();
-  }
-  uint32_t run = part[t] - s;
-  for (uint32_t k = lo; k < hi; ++k) {
-    const uint32_t c = A.blk[k];
-    A.blk[k] = run;
-    run += c;
-  }
-  if (t == 1023u) A.blk[A.nblk] = part[1023];
-}
-
-__global__ __launch_bounds__(256) void frag_index_kernel(FragArgs A) {
   __shared__ uint32_t wsum[4];
-  const uint32_t i = blockIdx.x * 256u + threadIdx.x, lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-  const bool c = i < A.P.n && frag_candidate(A.P, i);
-  const uint64_t m = __ballot(c);
-  if (lane == 0) wsum[w] = (uint32_t)__popcll(m);
-  __syncthreads();
-  if (c) {
-    uint32_t r = A.blk[blockIdx.x];
-    for (uint32_t k = 0; k < w; ++k) r += wsum[k];
-    A.idx[r + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = i;
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  const uint32_t base = blockIdx.x * kFragBlock;
+  uint32_t c = 0;
+#pragma unroll 2
+  for (uint32_t r = 0; r < kFragBlock / 256u; ++r) {
+    const uint32_t i = base + r * 256u + threadIdx.x;
+    const uint64_t m = __ballot(i < A.P.n && frag_candidate(A.P, i));
+    if (lane == 0 && base + r * 256u + w * 64u < A.P.n) A.mask[(base + r * 256u) / 64u + w] = m;
+    c += (uint32_t)__popcll(m);
   }
+  if (lane == 0) wsum[w] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) A.blk[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+
+// One workgroup: exclusive scan of the per-block counts in place, 1024 at a time (coalesced);
+// blk[nblk] = the total.
+__global__ __launch_bounds__(1024) void frag_scan_kernel(FragArgs A) {
+  __shared__ uint32_t wtot[16];
+  __shared__ uint32_t carry;
+  const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+  if (t == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t c0 = 0; c0 < A.nblk; c0 += 1024u) {
+    const uint32_t k = c0 + t;
+    const uint32_t v = k < A.nblk ? A.blk[k] : 0u;
+    uint32_t x = v;  // inclusive scan within the wave
+#pragma unroll
+    for (uint32_t d = 1; d < 64u; d <<= 1) {
+      const uint32_t y = __shfl_up(x, d, 64);
+      if (lane >= d) x += y;
+    }
+    if (lane == 63u) wtot[w] = x;
+    __syncthreads();
+    uint32_t before = carry;
+    for (uint32_t j = 0; j < w; ++j) before += wtot[j];
+    if (k < A.nblk) A.blk[k] = before + x - v;
+    __syncthreads();
+    if (t == 1023u) carry = before + x;
+    __syncthreads();
+  }
+  if (t == 0) A.blk[A.nblk] = carry;
+}
+
+// The candidates' packet indices in order, from the mask words: 32 words per block, one lane
+// each; a lane writes its word's set bits (fragments are rare: usually nothing at all).
+__global__ __launch_bounds__(64) void frag_index_kernel(FragArgs A) {
+  const uint32_t lane = threadIdx.x;
+  const uint32_t wi = blockIdx.x * (kFragBlock / 64u) + lane;
+  const uint32_t nw = (A.P.n + 63u) / 64u;
+  const uint64_t m = (lane < kFragBlock / 64u && wi < nw) ? A.mask[wi] : 0ull;
+  if (__ballot(m != 0ull) == 0ull) return;
+  uint32_t x = (uint32_t)__popcll(m), v = x;
+#pragma unroll
+  for (uint32_t d = 1; d < 64u; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  uint32_t r = A.blk[blockIdx.x] + x - v;
+  for (uint64_t b = m; b; b &= b - 1ull) A.idx[r++] = wi * 64u + (uint32_t)__builtin_ctzll(b);
 }
 
 // One lane per candidate: the generic decoder re-runs the packet for the IPv4 object's exact
@@ -2109,7 +2133,7 @@ hipError_t launch_ip4_frag(const FragArgs &A, hipStream_t stream, int num_cus) {
   if (A.nblk == 0) return hipSuccess;
   hipLaunchKernelGGL(frag_count_kernel, dim3(A.nblk), dim3(256), 0, stream, A);
   hipLaunchKernelGGL(frag_scan_kernel, dim3(1), dim3(1024), 0, stream, A);
-  hipLaunchKernelGGL(frag_index_kernel, dim3(A.nblk), dim3(256), 0, stream, A);
+  hipLaunchKernelGGL(frag_index_kernel, dim3(A.nblk), dim3(64), 0, stream, A);
   if (A.max_out == 0) return hipGetLastError();
   const size_t lds = (A.P.image_words * 4u + 15u) & ~15u;
   const unsigned grid = (unsigned)std::min<uint64_t>((uint64_t)num_cus * 2, (A.max_out + 255u) / 256u);

@@ -688,10 +688,11 @@ int gpd_ip4_fragments(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *res, 
   P.options = ctx->options;
   A.out = out;
   A.max_out = (uint32_t)std::min<uint64_t>(max_out, in->n);
-  A.nblk = (uint32_t)((in->n + 255) / 256);
+  A.nblk = (uint32_t)((in->n + 2047) / 2048);
   A.blk = static_cast<uint32_t *>(gpd::ctx_scratch(ctx, 12, ((size_t)A.nblk + 1) * 4));
   A.idx = static_cast<uint32_t *>(gpd::ctx_scratch(ctx, 13, (size_t)in->n * 4));
-  if (!A.blk || !A.idx) return set_err(GPD_ERR_NOMEM, "gpd_ip4_fragments: scratch allocation failed");
+  A.mask = static_cast<uint64_t *>(gpd::ctx_scratch(ctx, 14, ((size_t)in->n + 63) / 64 * 8));
+  if (!A.blk || !A.idx || !A.mask) return set_err(GPD_ERR_NOMEM, "gpd_ip4_fragments: scratch allocation failed");
   const hipStream_t s = (hipStream_t)stream;
   hipError_t e = gpd::launch_ip4_frag(A, s, ctx->num_cus);
   if (e != hipSuccess) return set_err(GPD_ERR_HIP, "gpd_ip4_fragments launch: %s", hipGetErrorString(e));

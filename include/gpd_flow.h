@@ -24,10 +24,11 @@
  *   gpd_flow_reset / gpd_flow_destroy                    (pool lifetime)
  *
  * The table is open addressing in HBM: 2^k records of 80 bytes; a record is claimed by a
- * 64-bit fingerprint of its key with one compare-and-swap, then every packet's full key is
- * compared with the record's stored key in a second pass, so a fingerprint collision is
- * detected (counted in gpd_flow_stats.collisions, the packet's flow id flagged) rather than
- * merging two flows silently.
+ * 56-bit fingerprint of its key (tagged with the claiming call's epoch) with one
+ * compare-and-swap, and every packet's full key is compared with the record's stored key — at
+ * once for records of earlier calls, in a second pass for records claimed in the same call —
+ * so a fingerprint collision is detected (counted in gpd_flow_stats.collisions, the packet's
+ * flow id flagged) rather than merging two flows silently.
  */
 #ifndef GPD_FLOW_H_
 #define GPD_FLOW_H_
@@ -39,7 +40,7 @@ extern "C" {
 
 /* One flow record (80 B, device memory; gpd_flow_export copies occupied ones out). */
 typedef struct gpd_flow_rec {
-  uint64_t fp;          /* key fingerprint; 0 = empty record */
+  uint64_t fp;          /* key fingerprint (56 bits); 0 = empty record */
   uint8_t  src[16];     /* NetworkFlow().Src() raw bytes (4 used for IPv4) */
   uint8_t  dst[16];     /* NetworkFlow().Dst() raw bytes */
   uint8_t  sport[2];    /* TransportFlow().Src() raw bytes (big-endian port) */
@@ -91,8 +92,8 @@ int gpd_flow_stats_get(gpd_flowtable *ft, gpd_flow_stats *out, void *stream);
 int gpd_flow_export(gpd_flowtable *ft, gpd_flow_rec *out, uint32_t *rec_index, uint64_t max,
                     uint64_t *n, void *stream);
 int gpd_flow_destroy(gpd_flowtable *ft);
-/* Testing hook: keep only the low `bits` (1..64) bits of every key fingerprint (64 = the
- * default) from the next insert on, so that distinct keys share fingerprints and the
+/* Testing hook: keep only the low `bits` (1..64) bits of every key fingerprint (56 or more =
+ * all 56, the default) from the next insert on, so that distinct keys share fingerprints and the
  * collision path (GPD_FLOW_COLLISION, gpd_flow_stats.collisions) runs.  Call it on an empty
  * table (after create or reset); a production table never calls it. */
 int gpd_flow_test_fingerprint_bits(gpd_flowtable *ft, uint32_t bits);

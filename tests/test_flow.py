@@ -357,3 +357,45 @@ def test_flow_counter_spills_are_exact(bits):
     flows_ref, per_ref = F.group(allp, ref)
     assert max(f["packets"] for f in flows_ref.values()) > 128
     _check_table(allp, None, np.concatenate(ids), ft, flows_ref, per_ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits", [3, 12])
+def test_flow_collisions_across_batches(bits):
+    """Records claimed by an earlier insert are updated and key-checked in the insert itself
+    (their epoch differs from the call's); with narrowed fingerprints the second batch's packets
+    land on the first batch's records and on their own, and every flag, the collision counter
+    and every record's counters must still match the restatement over both batches."""
+    import torch
+    from gopacket_amd import flows as FL
+    from gopacket_amd import parser as P
+    a, b = synth.make_mixed(12000, 0x5EED0101), _burst_batch(9000, 150, 9)
+    parser = P.NewDecodingLayerParser(L.LayerTypeEthernet, *[P.DECODER_BY_NAME[k]() for k in P.DECODER_BY_NAME])
+    ft = FL.NewFlowTable(parser, 1 << 16)
+    ft._test_fingerprint_bits(bits)
+    fids = []
+    for k, batch in enumerate((a, b, a)):
+        db, dr = _decode_dev(parser, batch)
+        fids.append(ft.Insert(db, dr, index_base=k * 20000).cpu().numpy().view(np.uint32))
+    torch.cuda.synchronize()
+    recs, idx = ft.Export()
+    st = ft.Stats()
+    stored = {int(ix): F.record_key(r) for r, ix in zip(recs, idx)}
+    flagged_total, on_rec = 0, {}
+    for k, (batch, fid) in enumerate(zip((a, b, a), fids)):
+        ref = O.decode(batch, L.LayerTypeEthernet, parser.decoders, 0, ext=False, nthreads=8)
+        _, per_ref = F.group(batch, ref)
+        keyed = np.array([x is not None for x in per_ref])
+        assert ((fid == 0xFFFFFFFF) == ~keyed).all()
+        rec_of = fid & 0x7FFFFFFF
+        flagged = (fid & 0x80000000) != 0
+        for i in np.nonzero(keyed)[0]:
+            assert flagged[i] == (per_ref[i] != stored[int(rec_of[i])])
+            on_rec.setdefault(int(rec_of[i]), []).append((k * 20000 + int(i), int(batch.caplen[i])))
+        flagged_total += int(flagged.sum())
+    assert st["collisions"] == flagged_total > 0 and st["full"] == 0
+    for r, ix in zip(recs, idx):
+        on = on_rec[int(ix)]
+        assert int(r["packets"]) == len(on)
+        assert int(r["bytes"]) == sum(c for _, c in on)
+        assert (int(r["first"]), int(r["last"])) == (min(s for s, _ in on), max(s for s, _ in on))
