@@ -74,10 +74,16 @@ struct KParams {
   uint32_t nstores;            // store instructions per tile (non-NULL result arrays)
   uint32_t fixed;              // tables in the kFix* layout (eth_mult shared by all three)
   uint32_t waves;              // fast kernel waves per SIMD (0: the default for the window)
-  uint32_t *fb_count;          // fast kernel: fallback list length (device scratch, zero)
-  uint32_t *fb_next;           // the counter the next fast launch uses (list_kernel zeroes it)
-  uint32_t *fb_list;           // fast kernel: packet indices left to the generic decoder
+  uint32_t *fb_count;          // fast kernel: 1 when any packet fell back (device scratch, zero)
+  uint32_t *fb_next;           // the flag the next fast launch uses (list_kernel zeroes it)
+  uint32_t *fb_list;           // fast kernel: packet indices left to the generic decoder, in one
+                               // private region per wave (64 x its tiles; see rs_kernel)
+  uint32_t *fb_wcount;         // per fast-kernel wave: entries in its region
+  uint32_t fb_waves;           // waves of the fast launch (set by launch_decode)
 };
+// Upper bound of the fast kernel's waves per launch, per compute unit (workgroups per CU x
+// grid rounds x 4 waves): sizes fb_wcount.
+constexpr uint32_t kMaxFastWavesPerCU = 4 * 4 * 4;
 
 // True when launch_decode takes the fast kernel + fallback list (needs fb_count/fb_list
 // with room for P.n entries).
@@ -156,7 +162,9 @@ constexpr uint64_t kMaxLaunchPackets = 1ull << 30;
 
 // Launch the decode kernel over P (asynchronous on `stream`).  `mid` (may be null) is
 // recorded between the fast kernel and the list kernel of the fallback packets.
-hipError_t launch_decode(const KParams &P, hipStream_t stream, int num_cus, hipEvent_t mid = nullptr);
+// *fb_waves (may be null) receives the fast kernel's wave count (0 for the generic kernel).
+hipError_t launch_decode(const KParams &P, hipStream_t stream, int num_cus, hipEvent_t mid = nullptr,
+                         uint32_t *fb_waves = nullptr);
 
 // Host side: set the thread's gpd_last_error_string() text and return `code` (gpd_runtime.cpp).
 int set_error(int code, const char *fmt, ...);

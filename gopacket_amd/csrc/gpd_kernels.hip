@@ -1670,7 +1670,17 @@ __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
                   (options & GPD_OPT_IGNORE_UNSUPPORTED) ? GPD_ST_OK : GPD_ST_UNSUPPORTED};
 
   uint32_t tp = blockIdx.x * WAVES + wave;  // the planner's tile
-  if (tp >= ntiles) return;
+  // Fallback list: wave w (tiles w, w + nwaves, ...) owns the region of 64 x its tile count
+  // that starts after the regions of waves 0..w-1, so its appends need no atomic (a shared
+  // counter took one same-address atomic per tile with leftovers; on the traffic mix that is
+  // every tile, serialised at the memory side); list_kernel reads each wave's count.
+  const uint32_t gw = tp;
+  const uint32_t fb_start = 64u * (gw * (ntiles / nwaves) + min(gw, ntiles % nwaves));
+  uint32_t fb_c = 0;
+  if (tp >= ntiles) {
+    if (lane == 0u) P.fb_wcount[gw] = 0u;
+    return;
+  }
   auto dload = [&](uint32_t u, uint32_t &o, uint32_t &c) {  // descriptors of tile u
     const uint32_t i = u * 64u + lane;
     o = c = 0;
@@ -1855,11 +1865,9 @@ __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
       got = 0;
       const uint64_t m = __ballot(fb != 0);  // the tile's leftovers go to the fallback list
       if (m) {
-        uint32_t base = 0;
-        if (lane == (uint32_t)__builtin_ctzll(m)) base = atomicAdd(P.fb_count, (uint32_t)__popcll(m));
-        base = __builtin_amdgcn_readlane(base, (int)__builtin_ctzll(m));
-        if (fb) P.fb_list[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                      __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = i;
+        if (fb) P.fb_list[fb_start + fb_c + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                               __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = i;
+        fb_c += (uint32_t)__popcll(m);
       }
       fb = 0;
       if (DEFER) {
@@ -1890,15 +1898,20 @@ __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
     Wd = Wn;
     cov_d = cov_n;
   }
+  if (lane == 0u) {
+    P.fb_wcount[gw] = fb_c;
+    if (fb_c) *P.fb_count = 1u;  // a plain store: every writer stores the same value
+  }
 }
 
 // The fallback list of the fast kernel: one lane per listed packet, bytes straight from
 // global memory (these packets are rare outside crafted inputs).
+// The fast kernel's waves' regions (rs_kernel): one wave here per wave there, grid-stride.
 template <bool PAGES>
 __global__ __launch_bounds__(256) void list_kernel(KParams P) {
-  const uint32_t cnt = *P.fb_count;
+  const uint32_t any = *P.fb_count;
   if (blockIdx.x == 0 && threadIdx.x == 0) *P.fb_next = 0;  // for the next fast launch
-  if (cnt <= blockIdx.x * 256u) return;  // nothing for this workgroup (usually: nothing at all)
+  if (!any) return;  // usually: nothing fell back
   for (uint32_t k = threadIdx.x; k < P.image_words; k += 256)
     reinterpret_cast<uint32_t *>(g_lds)[k] = P.image[k];
   __syncthreads();
@@ -1906,11 +1919,18 @@ __global__ __launch_bounds__(256) void list_kernel(KParams P) {
                      P.tcp_bits, P.udp_bits, P.eth_mult, P.tcp_mult, P.udp_mult};
   const uint32_t dlen = (uint32_t)P.data_len;
   const uint32_t options = P.options & ~kDiagMask;
-  for (uint32_t j = blockIdx.x * 256u + threadIdx.x; j < cnt; j += gridDim.x * 256u) {
-    const uint32_t i = P.fb_list[j];
-    const uint32_t off = min(P.offset[i], dlen);
-    const uint32_t len = min(P.caplen[i], dlen - off);
-    store_out(P, i, decode_packet<false>(GlbSrc{P.data, off}, len, T, P.first, options, nullptr));
+  const uint32_t n = P.n_dev ? min((uint32_t)P.n, *P.n_dev) : (uint32_t)P.n;
+  const uint32_t ntiles = (n + 63u) >> 6, nw = P.fb_waves;
+  const uint32_t lane = threadIdx.x & 63u;
+  for (uint32_t v = blockIdx.x * 4u + (threadIdx.x >> 6); v < nw; v += gridDim.x * 4u) {
+    const uint32_t c = P.fb_wcount[v];
+    const uint32_t start = 64u * (v * (ntiles / nw) + min(v, ntiles % nw));
+    for (uint32_t j = lane; j < c; j += 64u) {
+      const uint32_t i = P.fb_list[start + j];
+      const uint32_t off = min(P.offset[i], dlen);
+      const uint32_t len = min(P.caplen[i], dlen - off);
+      store_out(P, i, decode_packet<false>(GlbSrc{P.data, off}, len, T, P.first, options, nullptr));
+    }
   }
 }
 
@@ -1931,14 +1951,16 @@ static hipError_t launch_t(const KParams &P, hipStream_t stream, int num_cus) {
 }
 
 template <int STAGE, bool CS, bool HASH, int MINW, bool DEFER = false, bool RPFX = true, bool HO = false>
-static hipError_t launch_rs(const KParams &P, hipStream_t stream, int num_cus) {
+static hipError_t launch_rs(KParams &P, hipStream_t stream, int num_cus) {
   const uint64_t ntiles = (P.n + 63) / 64;
   const size_t lds = ((P.image_words * 4u + 15u) & ~15u) + 4 * (size_t)rs_wave_lds_bytes(STAGE) + 64;
   const uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>((160u * 1024u) / lds, MINW));
   uint64_t blocks = (ntiles + 3) / 4;
   const uint64_t cap = (uint64_t)num_cus * per_cu * kGridRounds;  // rounds of resident workgroups
   if (blocks > cap) blocks = cap;
+  P.fb_waves = (uint32_t)blocks * 4u;
   if (blocks == 0) return hipSuccess;
+  if (P.fb_waves > (uint32_t)num_cus * kMaxFastWavesPerCU) return hipErrorInvalidValue;
   hipLaunchKernelGGL((rs_kernel<STAGE, CS, HASH, MINW, DEFER, RPFX, HO>), dim3((unsigned)blocks), dim3(256), lds, stream, P);
   return hipGetLastError();
 }
@@ -1948,7 +1970,7 @@ static hipError_t launch_rs(const KParams &P, hipStream_t stream, int num_cus) {
 // spills.  The register-computed chunk prefix pays off for long frames only (IMIX -3 %); with
 // small frames (pcap records, VXLAN) its extra registers and code cost 1-2 %.
 template <bool CS, bool HASH>
-static hipError_t launch_fast(const KParams &P, hipStream_t stream, int num_cus) {
+static hipError_t launch_fast(KParams &P, hipStream_t stream, int num_cus) {
   if (P.stage == 4096) {
     if (P.waves == 2) return launch_rs<4096, CS, HASH, 2>(P, stream, num_cus);
     if (P.waves == 3) return launch_rs<4096, CS, HASH, 3>(P, stream, num_cus);
@@ -2148,10 +2170,13 @@ bool fast_eligible(const KParams &P) {
          (P.decoders & GPD_DEC_ETHERNET);
 }
 
-hipError_t launch_decode(const KParams &P, hipStream_t stream, int num_cus, hipEvent_t mid) {
+hipError_t launch_decode(const KParams &P0, hipStream_t stream, int num_cus, hipEvent_t mid,
+                         uint32_t *fb_waves) {
+  KParams P = P0;
+  P.fb_waves = 0;
   if (P.n > kMaxLaunchPackets) return hipErrorInvalidValue;
   if (fast_eligible(P)) {
-    if (!P.fb_count || !P.fb_next || !P.fb_list) return hipErrorInvalidValue;
+    if (!P.fb_count || !P.fb_next || !P.fb_list || !P.fb_wcount) return hipErrorInvalidValue;
     hipError_t e;
     const bool cs = !(P.options & GPD_OPT_NO_CHECKSUMS), hash = !(P.options & GPD_OPT_NO_FLOW_HASH);
     e = cs ? (hash ? launch_fast<true, true>(P, stream, num_cus)
@@ -2159,6 +2184,7 @@ hipError_t launch_decode(const KParams &P, hipStream_t stream, int num_cus, hipE
            : (hash ? launch_fast<false, true>(P, stream, num_cus)
                    : launch_fast<false, false>(P, stream, num_cus));
     if (e != hipSuccess) return e;
+    if (fb_waves) *fb_waves = P.fb_waves;
     if (mid && (e = hipEventRecord(mid, stream)) != hipSuccess) return e;
     const size_t lds = (P.image_words * 4u + 15u) & ~15u;
     hipLaunchKernelGGL(list_kernel<false>, dim3((unsigned)num_cus * 2), dim3(256), lds, stream, P);

@@ -208,7 +208,8 @@ struct gpd_ctx {
   bool fixed = false;  // tables in the fixed layout the fast kernel compiles in
   // fast-kernel fallback lists, one per stream the context is used on (count + indices)
   struct Fallback {
-    uint32_t *d = nullptr;
+    uint32_t *d = nullptr;   // two flags (words 0 and 64), then the list
+    uint32_t *wc = nullptr;  // two arrays of per-wave counts (one per parity)
     uint64_t cap = 0;
     uint32_t parity = 0;
   };
@@ -223,7 +224,8 @@ struct gpd_ctx {
   hipEvent_t ev0 = nullptr, ev1 = nullptr, evm = nullptr;
   bool timed = false;
   bool timed_split = false;           // evm marks the fast kernel's end in the timed launch
-  uint32_t *timed_fb_count = nullptr;  // its fallback counter (device)
+  const uint32_t *timed_fb_wc = nullptr;  // its per-wave fallback counts (device)
+  uint32_t timed_fb_waves = 0;
   // gpd_decode_host staging (two slots)
   struct Slot {
     hipStream_t stream = nullptr;
@@ -443,8 +445,10 @@ int gpd_ctx_destroy(gpd_ctx *ctx) {
   free_slots(ctx);
   if (ctx->d_image) (void)hipFree(ctx->d_image);
   if (ctx->d_pages) (void)hipFree(ctx->d_pages);
-  for (auto &kv : ctx->fallback)
+  for (auto &kv : ctx->fallback) {
     if (kv.second.d) (void)hipFree(kv.second.d);
+    if (kv.second.wc) (void)hipFree(kv.second.wc);
+  }
   for (auto &sc : ctx->scratch)
     if (sc.d) (void)hipFree(sc.d);
   for (const auto &r : ctx->registered) (void)hipHostUnregister((void *)r.first);
@@ -465,8 +469,12 @@ int gpd_last_launch_split(gpd_ctx *ctx, uint64_t *fallback, float *fast_ms, floa
   HIP_TRY(hipEventSynchronize(ctx->ev1));
   HIP_TRY(hipEventElapsedTime(fast_ms, ctx->ev0, ctx->evm));
   HIP_TRY(hipEventElapsedTime(list_ms, ctx->evm, ctx->ev1));
-  uint32_t c = 0;  // the launch's counter stays until the launch after next zeroes it
-  HIP_TRY(hipMemcpy(&c, ctx->timed_fb_count, sizeof c, hipMemcpyDeviceToHost));
+  // the launch's per-wave counts stay until the launch after next on the stream rewrites them
+  std::vector<uint32_t> wc(ctx->timed_fb_waves);
+  if (!wc.empty())
+    HIP_TRY(hipMemcpy(wc.data(), ctx->timed_fb_wc, wc.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  uint64_t c = 0;
+  for (uint32_t v : wc) c += v;
   *fallback = c;
   return GPD_OK;
 }
@@ -590,11 +598,14 @@ static int launch(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, hipS
       if (fb.d) {
         HIP_TRY(hipStreamSynchronize(stream));
         HIP_TRY(hipFree(fb.d));
-        fb.d = nullptr;
+        HIP_TRY(hipFree(fb.wc));
+        fb.d = fb.wc = nullptr;
         fb.cap = 0;
       }
-      HIP_TRY(hipMalloc(&fb.d, (need + 128) * sizeof(uint32_t)));
-      HIP_TRY(hipMemset(fb.d, 0, 128 * sizeof(uint32_t)));  // both counters start at zero
+      // the list: 64 entries per tile (each wave's region spans its tiles), after the flags
+      HIP_TRY(hipMalloc(&fb.d, (need + 64 + 128) * sizeof(uint32_t)));
+      HIP_TRY(hipMemset(fb.d, 0, 128 * sizeof(uint32_t)));  // both flags start at zero
+      HIP_TRY(hipMalloc(&fb.wc, 2ull * ctx->num_cus * gpd::kMaxFastWavesPerCU * sizeof(uint32_t)));
       fb.cap = need;
       fb.parity = 0;
     }
@@ -621,11 +632,16 @@ static int launch(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, hipS
       auto &fb = ctx->fallback[stream];  // list kernel zeroes the one the next launch takes
       Q.fb_count = fb.d + 64 * fb.parity;
       Q.fb_next = fb.d + 64 * (fb.parity ^ 1u);
+      Q.fb_wcount = fb.wc + (size_t)ctx->num_cus * gpd::kMaxFastWavesPerCU * fb.parity;
       fb.parity ^= 1u;
     }
-    hipError_t e = gpd::launch_decode(Q, stream, ctx->num_cus, split ? ctx->evm : nullptr);
+    uint32_t fbw = 0;
+    hipError_t e = gpd::launch_decode(Q, stream, ctx->num_cus, split ? ctx->evm : nullptr, &fbw);
     if (e != hipSuccess) return set_err(GPD_ERR_HIP, "decode kernel launch: %s", hipGetErrorString(e));
-    if (split) ctx->timed_fb_count = Q.fb_count;
+    if (split) {
+      ctx->timed_fb_wc = Q.fb_wcount;
+      ctx->timed_fb_waves = fbw;
+    }
   }
   if (record) {
     HIP_TRY(hipEventRecord(ctx->ev1, stream));
