@@ -221,14 +221,16 @@ def summarize(workload, n, world, steps, warmup, elapsed, kern_ms, kern_ms_max, 
     }
 
 
-def bench_record36(parser, dev_batch, n, local, stream, out, args, records=False, soa=False):
-    """The same launch writing the 36-B record: the five SoA arrays plus hdr_off (the
-    NetworkFlow / TransportFlow header offsets the F3 flow table reads).  Event-timed like the
-    metric.  records=True: the 32-B record as one gpd_record per packet (AoS); soa=True: the
-    32-B record as the five SoA arrays."""
+def bench_record36(parser, dev_batch, n, local, stream, out, args, records=False, soa=False, hdr=None):
+    """The same launch writing the 36-B record: the five SoA arrays (or, records=True, one
+    gpd_record per packet) plus hdr_off (the NetworkFlow / TransportFlow header offsets the F3
+    flow table reads).  Event-timed like the metric.  soa=True / records=True without hdr: the
+    32-B record as the five SoA arrays / as gpd_records."""
     import torch
     from gopacket_amd import parser as P
-    res = P.DeviceResult(n, local, ext=False, hdr_off=not (records or soa), records=records)
+    if hdr is None:
+        hdr = not (records or soa)
+    res = P.DeviceResult(n, local, ext=False, hdr_off=hdr, records=records)
     for _ in range(3):
         parser.decode_device(dev_batch, res, stream)
     k = max(5, min(args.steps, 20))
@@ -240,7 +242,7 @@ def bench_record36(parser, dev_batch, n, local, stream, out, args, records=False
     torch.cuda.synchronize(local)
     ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     rb = out["roofline"]["algorithmic_read_bytes"]
-    wb = 32 if (records or soa) else 36
+    wb = 36 if hdr else 32
     alg = rb + wb * n
     del res
     return {"result_bytes_per_packet": wb, "kernel_ms": round(ms, 4),
@@ -1025,7 +1027,12 @@ def main():
     out["config"]["result_form"] = "gpd_record (AoS)" if aos else "SoA arrays"
     out["config"]["settle_ms"] = settled
     if not args.ablate and not args.lean:  # the 36-B record (hdr_off on, as the flow table uses)
+        # the five SoA arrays + hdr_off (the decode -> flow table pipeline's form); gpd_records +
+        # hdr_off beside it (gpd_flow_insert takes either; measured slower on this part)
         out["record36"] = bench_record36(parser, dev_batch, n, local, stream, out, args)
+        out["record36"]["form"] = "SoA arrays + hdr_off"
+        out["record36_aos"] = bench_record36(parser, dev_batch, n, local, stream, out, args, records=True, hdr=True)
+        out["record36_aos"]["form"] = "gpd_record + hdr_off"
         if aos:  # the same launch writing the five SoA arrays
             out["record_soa"] = bench_record36(parser, dev_batch, n, local, stream, out, args, soa=True)
         else:

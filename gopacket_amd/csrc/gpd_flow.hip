@@ -75,13 +75,14 @@ struct FlowParams {
   uint64_t *made = nullptr;
   uint64_t fp_mask = kFpBits;  // gpd_flow_test_fingerprint_bits (kFpBits in production)
   uint32_t cbits = kCountBits;  // gpd_flow_test_counter_bits (kCountBits in production)
+  const gpd_record *rec = nullptr;  // results in the gpd_record form (status and hashes there)
   uint64_t tag = 1ull << 56;    // this launch's epoch (1..255) in the fingerprint word's top byte
 };
 
 // The key of packet i as 10 words: src[16], dst[16], ports (raw wire bytes), types.  Returns
 // false when the packet has no network + transport pair (gpd.h status / hdr_off words).
 __device__ __forceinline__ bool flow_key(const FlowParams &P, uint64_t i, uint32_t (&k)[10]) {
-  const uint32_t st = P.status[i], ho = P.hdr_off[i];
+  const uint32_t st = P.rec ? P.rec[i].status : P.status[i], ho = P.hdr_off[i];
   const uint32_t nt = (st >> 20) & 15u, tt = (st >> 24) & 15u;
   const uint32_t no = ho & 0xFFFFu, to = ho >> 16;
   if (nt == 0 || tt == 0 || no == 0xFFFFu || to == 0xFFFFu) return false;
@@ -382,7 +383,7 @@ __global__ __launch_bounds__(kFlowThreads) void flow_verify_kernel(FlowParams P)
 // Owner rank of a keyed packet: the high half of the two direction-symmetric FastHashes'
 // xor, scaled to [0, nparts) (doc.go:216-228 picks a worker by flow.FastHash()).
 __device__ __forceinline__ uint32_t flow_owner(const FlowParams &P, uint64_t i) {
-  const uint64_t h = P.net_hash[i] ^ P.tp_hash[i];
+  const uint64_t h = P.rec ? P.rec[i].net_hash ^ P.rec[i].tp_hash : P.net_hash[i] ^ P.tp_hash[i];
   return (uint32_t)(((h >> 32) * (uint64_t)P.nparts) >> 32);
 }
 
@@ -632,8 +633,8 @@ int gpd_flow_insert(gpd_flowtable *ft, const gpd_batch *in, const gpd_result *re
                     uint32_t *flow_id, uint64_t index_base, void *stream) {
   if (!ft || !in || !res || !flow_id)
     return gpd::set_error(GPD_ERR_INVALID, "gpd_flow_insert: null argument");
-  if (!res->status || !res->hdr_off)
-    return gpd::set_error(GPD_ERR_INVALID, "gpd_flow_insert: the results need status and hdr_off");
+  if (!(res->status || res->records) || !res->hdr_off)
+    return gpd::set_error(GPD_ERR_INVALID, "gpd_flow_insert: the results need status (or records) and hdr_off");
   if (in->n == 0) return GPD_OK;
   if (!in->data || !in->offset || !in->caplen)
     return gpd::set_error(GPD_ERR_INVALID, "gpd_flow_insert: null batch array");
@@ -644,6 +645,7 @@ int gpd_flow_insert(gpd_flowtable *ft, const gpd_batch *in, const gpd_result *re
   FLOW_TRY(grow_made(ft, in->n));
   P.made = ft->made;
   P.fp_mask = ft->fp_mask;
+  P.rec = res->records;
   P.cbits = ft->cbits;
   P.tag = next_tag(ft);
   hipStream_t s = (hipStream_t)stream;
@@ -662,9 +664,9 @@ int gpd_flow_keys(gpd_flowtable *ft, const gpd_batch *in, const gpd_result *res,
   if (nparts == 0 || nparts > GPD_FLOW_MAX_PARTS)
     return gpd::set_error(GPD_ERR_INVALID, "gpd_flow_keys: nparts %u outside [1, %d]", nparts,
                           GPD_FLOW_MAX_PARTS);
-  if (!res->status || !res->hdr_off || !res->net_hash || !res->tp_hash)
+  if (!res->hdr_off || !(res->records || (res->status && res->net_hash && res->tp_hash)))
     return gpd::set_error(GPD_ERR_INVALID,
-                          "gpd_flow_keys: the results need status, hdr_off, net_hash and tp_hash");
+                          "gpd_flow_keys: the results need hdr_off and records, or status, net_hash and tp_hash");
   for (uint32_t p = 0; p < nparts; p++) part_count[p] = 0;
   if (in->n == 0) return GPD_OK;
   if (!in->data || !in->offset || !in->caplen)
@@ -684,6 +686,7 @@ int gpd_flow_keys(gpd_flowtable *ft, const gpd_batch *in, const gpd_result *res,
                     nullptr, in->n, index_base, ft->tab, ft->cap - 1, ft->stats,
                     nullptr, res->net_hash, res->tp_hash, keys, ft->parts, nparts};
   P.fp_mask = ft->fp_mask;
+  P.rec = res->records;
   hipLaunchKernelGGL(gpd::flow_part_count_kernel, grid, block, 0, s, P);
   FLOW_TRY(hipGetLastError());
   hipLaunchKernelGGL(gpd::flow_part_scan_kernel, dim3(1), dim3(1024), 0, s, ft->parts, L, nparts, grid.x);

@@ -65,7 +65,7 @@ class FlowTable:
         if dres.hdr_off is None:
             raise ValueError("FlowTable.Insert needs a DeviceResult with hdr_off")
         if flow_id is None:
-            flow_id = torch.empty(dbatch.n, dtype=torch.int32, device=dres.status.device)
+            flow_id = torch.empty(dbatch.n, dtype=torch.int32, device=dres.hdr_off.device)
         b, r = dbatch.c_batch(), dres.c_result()
         check(lib.gpd_flow_insert(self.h, C.byref(b), C.byref(r), C.c_void_p(flow_id.data_ptr()),
                                   int(index_base), self._stream(stream)), "gpd_flow_insert")
@@ -177,7 +177,7 @@ class ShardedFlowTable:
         t = self.table
         if dres.hdr_off is None:
             raise ValueError("ShardedFlowTable.Insert needs a DeviceResult with hdr_off")
-        dev = dres.status.device
+        dev = dres.hdr_off.device
         t0 = time.perf_counter()
         keys = torch.empty((max(dbatch.n, 1), KEY_WORDS), dtype=torch.int64, device=dev)
         counts = (C.c_uint64 * self.world)()

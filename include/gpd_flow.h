@@ -80,7 +80,7 @@ int gpd_flow_create(gpd_ctx *ctx, uint64_t capacity, gpd_flowtable **out);
 /* Empty the table (asynchronous on `stream`). */
 int gpd_flow_reset(gpd_flowtable *ft, void *stream);
 /* Find-or-create the flow of every packet of a decoded batch (device pointers): `in` is the
- * batch gpd_decode read, `res` its results (status and hdr_off required), flow_id[n] receives
+ * batch gpd_decode read, `res` its results (hdr_off, and status or the gpd_record form), flow_id[n] receives
  * each packet's record index (or a GPD_FLOW_* value).  Packet i counts as sequence number
  * index_base + i.  Asynchronous on `stream`; the batch must be decoded on that stream first. */
 int gpd_flow_insert(gpd_flowtable *ft, const gpd_batch *in, const gpd_result *res,
@@ -123,8 +123,8 @@ typedef struct gpd_flow_key {
 
 /* Key records of every packet of a decoded device batch that has a network + transport pair,
  * grouped by owner: partition p occupies keys[start_p, start_p + part_count[p]) with start_p
- * the sum of the counts below p.  `res` needs status, hdr_off, net_hash and tp_hash (decode
- * without GPD_OPT_NO_FLOW_HASH); `keys` (device) holds in->n records; part_count (host,
+ * the sum of the counts below p.  `res` needs hdr_off and either the gpd_record form or status,
+ * net_hash and tp_hash (decode without GPD_OPT_NO_FLOW_HASH); `keys` (device) holds in->n records; part_count (host,
  * nparts entries) is filled when the call returns (it synchronises `stream`: the counts size
  * the exchange).  Order within a partition is unspecified.  1 <= nparts <= GPD_FLOW_MAX_PARTS. */
 int gpd_flow_keys(gpd_flowtable *ft, const gpd_batch *in, const gpd_result *res, uint32_t nparts,

@@ -1,5 +1,6 @@
 """F3 flow table (include/gpd_flow.h): the GPU connection map vs the CPU restatement of
 tcpassembly's key{NetworkFlow(), TransportFlow()} grouping (oracle/flow_ref.py)."""
+import ctypes as C
 import os
 import sys
 
@@ -399,3 +400,36 @@ def test_flow_collisions_across_batches(bits):
         assert int(r["packets"]) == len(on)
         assert int(r["bytes"]) == sum(c for _, c in on)
         assert (int(r["first"]), int(r["last"])) == (min(s for s, _ in on), max(s for s, _ in on))
+
+
+@pytest.mark.gpu
+def test_flow_table_reads_the_record_form():
+    """A batch decoded into gpd_records + hdr_off inserts, keys and shards exactly as the same
+    batch decoded into the SoA arrays (status and hashes read from the records)."""
+    import torch
+    from gopacket_amd import flows as FL
+    from gopacket_amd import parser as P
+    batch = _burst_batch(12000, 300, 13)
+    parser = P.NewDecodingLayerParser(L.LayerTypeEthernet, *[P.DECODER_BY_NAME[k]() for k in P.DECODER_BY_NAME])
+    got = []
+    for records in (False, True):
+        db = P.DeviceBatch(batch, 0)
+        dr = P.DeviceResult(batch.n, 0, records=records)
+        parser.decode_device(db, dr)
+        ft = FL.NewFlowTable(parser, 1 << 15)
+        fid = ft.Insert(db, dr).cpu().numpy().view(np.uint32)
+        recs, idx = ft.Export()
+        st = ft.Stats()
+        keys = torch.empty(batch.n * 64, dtype=torch.uint8, device="cuda")
+        counts = (C.c_uint64 * 3)()
+        b, r = db.c_batch(), dr.c_result()
+        FL.check(FL.lib.gpd_flow_keys(ft.h, C.byref(b), C.byref(r), 3, 0, C.c_void_p(keys.data_ptr()),
+                                      counts, ft._stream(None)), "gpd_flow_keys")
+        m = int(sum(counts))
+        kr = keys[:m * 64].cpu().numpy().view(FL.FLOW_KEY_DTYPE)
+        torch.cuda.synchronize()
+        got.append((fid, recs, idx, st, list(counts), np.sort(kr["seq"]), kr))
+    a, b2 = got
+    assert np.array_equal(a[0], b2[0]) and np.array_equal(a[1], b2[1]) and np.array_equal(a[2], b2[2])
+    assert a[3] == b2[3] and a[4] == b2[4] and np.array_equal(a[5], b2[5])
+    assert np.array_equal(np.sort(a[6], order="seq"), np.sort(b2[6], order="seq"))
