@@ -2187,7 +2187,10 @@ hipError_t launch_decode(const KParams &P0, hipStream_t stream, int num_cus, hip
     if (fb_waves) *fb_waves = P.fb_waves;
     if (mid && (e = hipEventRecord(mid, stream)) != hipSuccess) return e;
     const size_t lds = (P.image_words * 4u + 15u) & ~15u;
-    hipLaunchKernelGGL(list_kernel<false>, dim3((unsigned)num_cus * 2), dim3(256), lds, stream, P);
+    // one list wave per fast wave: a region's packets decode one lane each, latency-bound (a
+    // chain of dependent header loads), so every region gets its own wave
+    hipLaunchKernelGGL(list_kernel<false>, dim3(std::max<unsigned>((unsigned)num_cus * 2, (P.fb_waves + 3u) / 4u)),
+                       dim3(256), lds, stream, P);
     return hipGetLastError();
   }
   if (P.ext) return P.use_pages ? launch_s<true, true>(P, stream, num_cus)
