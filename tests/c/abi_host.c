@@ -15,8 +15,12 @@
  * and then the device results feed the flow table (gpd_flow_insert on the caller's stream):
  * every packet's flow record must hold exactly the key bytes at the packet's hdr_off
  * positions, the per-record packet/byte/first/last counters must match a recount, records
- * must have pairwise distinct keys, and gpd_flow_stats must add up.
- * Prints "abi_host ok N F" (F = flows) and exits 0 when everything agrees bit for bit.
+ * must have pairwise distinct keys, and gpd_flow_stats must add up.  Last, the fragment
+ * hand-off (gpd_ip4_fragments) over the same device results: its records must be exactly the
+ * packets whose last network layer is an IPv4 header with MoreFragments or an offset and no
+ * DF, in packet order, with the key and fields of those header bytes and the securityChecks
+ * verdict (ip4defrag/defrag.go:162-198) recomputed here.
+ * Prints "abi_host ok N F R" (F = flows, R = fragments) and exits 0 when everything agrees.
  */
 #include <stddef.h>
 #include <stdint.h>
@@ -27,6 +31,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include "../../include/gpd.h"
+#include "../../include/gpd_defrag.h"
 #include "../../include/gpd_flow.h"
 #include "../../include/gpd_pcap.h"
 #include "../../oracle/gpd_oracle.h"
@@ -189,6 +194,52 @@ static uint8_t *make_pcap(const uint8_t *data, const uint32_t *off, const uint32
   return b;
 }
 
+/* gpd_ip4_fragments vs a recount from the oracle's status / header-offset words and the bytes */
+static int check_fragments(gpd_ctx *ctx, hipStream_t s, const gpd_batch *db, const gpd_result *dr,
+                           const uint8_t *data, const uint32_t *off, const uint32_t *cap,
+                           const uint32_t *status, const uint32_t *hdr_off, uint64_t n, uint64_t *nfrag) {
+  gpd_ip4_frag *d_out = NULL;
+  HCHECK(hipMalloc((void **)&d_out, sizeof(gpd_ip4_frag) * (n + 1)));
+  uint64_t cnt = 0;
+  CHECK(gpd_ip4_fragments(ctx, db, dr, d_out, n, &cnt, s));
+  gpd_ip4_frag *fr = calloc(cnt + 1, sizeof(gpd_ip4_frag));
+  HCHECK(hipMemcpy(fr, d_out, sizeof(gpd_ip4_frag) * cnt, hipMemcpyDeviceToHost));
+  HCHECK(hipFree(d_out));
+  uint64_t k = 0;
+  int bad = 0;
+  for (uint64_t i = 0; i < n && !bad; i++) {
+    const uint32_t net = GPD_HDR_NET(hdr_off[i]);
+    if (GPD_STATUS_NET_EPT(status[i]) != 1 || net == GPD_HDR_NONE) continue;
+    const uint8_t *h = data + off[i] + net;
+    const uint32_t ff = ((uint32_t)h[6] << 8) | h[7], flags = ff >> 13, fo = ff & 0x1FFF;
+    if ((flags & 2) || (!(flags & 1) && fo == 0)) continue; /* dontDefrag */
+    if (k >= cnt) { fprintf(stderr, "fragments: packet %llu missing\n", (unsigned long long)i); bad = 1; break; }
+    const gpd_ip4_frag *r = &fr[k++];
+    const uint32_t raw = ((uint32_t)h[2] << 8) | h[3], ihl = h[0] & 15u;
+    const uint32_t id = ((uint32_t)h[4] << 8) | h[5];
+    int ok = r->packet == i && r->net_off == net && memcmp(r->src, h + 12, 4) == 0 &&
+             memcmp(r->dst, h + 16, 4) == 0 && r->id == id && r->frag_offset == fo && r->flags == flags &&
+             r->ihl == ihl && net + 4 * ihl + r->payload_len <= cap[i];
+    if (raw) {
+      const uint16_t size = (uint16_t)(raw - 4 * ihl);
+      const uint32_t v = size < 8 ? GPD_FRAG_TOO_SMALL : fo > 8183 ? GPD_FRAG_OFFSET : GPD_FRAG_INSERT;
+      ok = ok && r->length == raw && r->verdict == v;
+    }
+    if (!ok) {
+      fprintf(stderr, "fragments: record %llu (packet %llu) disagrees\n", (unsigned long long)(k - 1),
+              (unsigned long long)i);
+      bad = 1;
+    }
+  }
+  if (!bad && k != cnt) {
+    fprintf(stderr, "fragments: %llu records, %llu expected\n", (unsigned long long)cnt, (unsigned long long)k);
+    bad = 1;
+  }
+  free(fr);
+  *nfrag = cnt;
+  return bad;
+}
+
 int main(int argc, char **argv) {
   if (argc != 2) {
     fprintf(stderr, "usage: %s BATCH_FILE\n", argv[0]);
@@ -284,9 +335,14 @@ int main(int argc, char **argv) {
   uint64_t flows = 0;
   if (!bad && n > 0) bad |= check_flows(ctx, s, &db, &dr, data, off, cap, ov.hdr_off, n, &flows);
 
+  /* 6. the fragment hand-off over the same device results */
+  uint64_t frags = 0;
+  if (!bad && n > 0) bad |= check_fragments(ctx, s, &db, &dr, data, off, cap, ov.status, ov.hdr_off, n, &frags);
+
   CHECK(gpd_ctx_destroy(ctx));
   HCHECK(hipStreamDestroy(s));
   if (bad) return 1;
-  printf("abi_host ok %llu %llu\n", (unsigned long long)n, (unsigned long long)flows);
+  printf("abi_host ok %llu %llu %llu\n", (unsigned long long)n, (unsigned long long)flows,
+         (unsigned long long)frags);
   return 0;
 }

@@ -105,6 +105,8 @@ def test_c_host_program_on_the_abi(tmp_path):
     pkts += [p[:k] for p in pkts[:8] for k in range(0, len(p), 3)]
     mixed = synth.make_mixed(3000)
     pkts += [mixed.packet(i) for i in range(mixed.n)]
+    import test_defrag as TD  # the ip4defrag fixtures and fragment fuzz frames
+    pkts += list(TD._frames().values()) + [f for _, f in TD.struct_frames()] + TD.fuzz_frames(600, 5)
     for decoders, options in ((0xFFF, 0), (0x3FF, 1), (0x1 | 0x4 | 0x400 | 0x20 | 0x40 | 0x100, 0)):
         b = PacketBatch.from_packets(pkts)
         f = tmp_path / f"batch_{decoders:x}_{options}.bin"
@@ -119,3 +121,4 @@ def test_c_host_program_on_the_abi(tmp_path):
         words = r.stdout.split()
         assert words[:3] == ["abi_host", "ok", str(b.n)], r.stdout
         assert int(words[3]) > 100, r.stdout  # the mixed traffic holds many TCP/UDP flows
+        assert int(words[4]) > 100, r.stdout  # ip4defrag's fragments and the fuzz frames
