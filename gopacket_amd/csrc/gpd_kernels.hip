@@ -1390,6 +1390,9 @@ __host__ __device__ constexpr uint32_t wave_lds_bytes(int stage, bool fast) {
 template <int STAGE, bool FAST, bool EXT, bool PAGES, bool SWZ, int WAVES, bool CS = true,
           bool HASH = true, int MINW = 1>
 __global__ __launch_bounds__(64 * WAVES, MINW) void decode_kernel(KParams P) {
+  // The fast path is rs_kernel, whose fallback list is per-wave regions (list_kernel reads
+  // those); this loop's FAST form appended to one shared counter and is no longer launched.
+  static_assert(!FAST, "decode_kernel<FAST> predates the per-wave fallback regions");
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // stage the dispatch-table image (LUT, ipproto, hashes) into LDS
