@@ -265,3 +265,25 @@ def test_fragment_empty_and_fragment_free_batches():
     db = P.DeviceBatch(PacketBatch.from_packets([]), 0)
     dr = P.DeviceResult(0, 0)
     assert DF.IPv4Fragments(parser, db, dr)[1] == 0
+
+
+@pytest.mark.gpu
+def test_fragment_header_past_the_offset_word():
+    """An IPv4 header past byte 65534 (16,384 802.1Q tags in front of it): the header offsets
+    word saturates, so the batch pass cannot rule the packet out from the header bytes and the
+    record pass decides — a fragment is handed over exactly as the oracle restates it, a
+    non-fragment comes back as one GPD_FRAG_WHOLE record (DefragIPv4 would return it as is)."""
+    frag = ip4_frame(600, 1, 0, 0x1234, tags=16384)
+    whole = ip4_frame(600, 0, 0, 0x4321, tags=16384)
+    small = ip4_frame(600, 1, 10, 0x99)
+    batch = PacketBatch.from_packets([small, frag, whole, small])
+    parser = _all_parser()
+    ref = D.ip4_fragments(batch, O.decode(batch, L.LayerTypeEthernet, parser.decoders, 0, ext=True))
+    assert list(ref["packet"]) == [0, 1, 3]
+    got, cnt = _device_fragments(parser, batch)
+    assert cnt == 4
+    assert list(got["packet"]) == [0, 1, 2, 3]
+    keep = got["packet"] != 2
+    assert np.array_equal(got[keep].view(np.uint8), ref.view(np.uint8))
+    w = got[~keep][0]
+    assert w["verdict"] == D.FRAG_WHOLE and w["net_off"] == 14 + 4 * 16384 and w["id"] == 0x4321
