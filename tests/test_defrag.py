@@ -287,3 +287,93 @@ def test_fragment_header_past_the_offset_word():
     assert np.array_equal(got[keep].view(np.uint8), ref.view(np.uint8))
     w = got[~keep][0]
     assert w["verdict"] == D.FRAG_WHOLE and w["net_off"] == 14 + 4 * 16384 and w["id"] == 0x4321
+
+
+# ---------------------------------------------------------------- the stateful rest (host)
+def _reassemble(order, recs_by_name, frames, t=1.0):
+    """Feed the handed-over records in `order` to one IPv4Defragmenter; returns the outcome of
+    each call (layer, error)."""
+    from gopacket_amd.ip4defrag import NewIPv4Defragmenter
+    d = NewIPv4Defragmenter()
+    return d, [d.DefragIPv4WithTimestamp(recs_by_name[k], frames[k], t) for k in order]
+
+
+def _defrag_scenarios(recs_by_name):
+    """ip4defrag/defrag_test.go's frame scenarios, asserted as the reference asserts them."""
+    fr = _frames()
+    a = VEC["asserted"]
+    want1 = b"".join(fr[f"testPing1Frag{k}"][a["payload_from"]:] for k in (1, 2, 3, 4))
+    want2 = b"".join(fr[f"testPing2Frag{k}"][a["payload_from"]:] for k in (1, 2, 3, 4))
+    # TestDefragPing1 (:69-104), twice on one defragmenter
+    order = ["testPing1Frag1", "testPing1Frag3", "testPing1Frag2", "testPing1Frag4"]
+    d, outs = _reassemble(order + order, recs_by_name, fr)
+    for k, (o, e) in enumerate(outs):
+        assert e is None and ((o is not None) == (k % 4 == 3)), (k, o, e)
+    assert len(outs[3][0].payload) == a["datagram_payload_len"] and outs[3][0].payload == want1
+    assert outs[7][0].payload == outs[3][0].payload
+    # TestDefragIDField (:245-259)
+    assert outs[3][0].ident == struct.unpack(">H", fr["testPing1Frag1"][18:20])[0]
+    # TestDefragPingMultipleFrags (:38-67): duplicates ignored, nothing left to discard
+    order = ["testPing1Frag1"] * 3 + ["testPing1Frag3", "testPing1Frag2", "testPing1Frag4"]
+    d, outs = _reassemble(order, recs_by_name, fr)
+    assert [o is not None for o, _ in outs] == [False] * 5 + [True] and outs[5][0].payload == want1
+    assert d.DiscardOlderThan(10.0) == 0
+    # TestDefragPing1and2 (:106-151)
+    order = a["ping1_and2_order"]
+    d, outs = _reassemble(order, recs_by_name, fr)
+    done = [k for k, (o, e) in zip(order, outs) if o is not None]
+    assert done == [a["completing"]["ping1"], a["completing"]["ping2_after_ping1_and2_order"]]
+    assert outs[order.index("testPing1Frag4")][0].payload == want1
+    assert outs[order.index("testPing2Frag2")][0].payload == want2
+    # TestDefragDiscard (:204-214)
+    d, outs = _reassemble(["testPing1Frag1", "testPing2Frag1"], recs_by_name, fr, t=1.0)
+    assert d.DiscardOlderThan(2.0) == 2
+
+
+def _struct_scenarios(recs, frames):
+    """TestDefragTooSmall / FragmentOffset / MaxSize (:153-243): each test's layers through one
+    defragmenter, errors where the reference expects them."""
+    from gopacket_amd.ip4defrag import NewIPv4Defragmenter
+    cases = [s for s, _ in struct_frames()]
+    by_test = {}
+    for k, s in enumerate(cases):
+        by_test.setdefault(s["test"].split()[0], []).append(k)
+    rec_of = {int(r["packet"]): r for r in recs}
+    for name, ks in by_test.items():
+        d = NewIPv4Defragmenter()
+        for k in ks:
+            if cases[k].get("unchanged"):
+                assert k not in rec_of
+                continue
+            out, err = d.DefragIPv4WithTimestamp(rec_of[k], frames[k], 1.0)
+            assert (err is not None) == cases[k]["error"], (cases[k]["test"], err)
+            if cases[k]["error"]:
+                assert err.startswith("defrag: fragment")
+
+
+def test_defragmenter_on_oracle_records():
+    """The host defragmenter over the oracle's hand-off records reproduces every outcome
+    defrag_test.go asserts (payload bytes, completing fragment, duplicates, discard, Id, the
+    security errors)."""
+    fr = _frames()
+    names = list(fr)
+    batch = PacketBatch.from_packets([fr[k] for k in names])
+    recs = D.ip4_fragments(batch, O.decode(batch, L.LayerTypeEthernet, ALL, 0, ext=True))
+    _defrag_scenarios({k: r for k, r in zip(names, recs)})
+    sf = [f for _, f in struct_frames()]
+    sb = PacketBatch.from_packets(sf)
+    _struct_scenarios(D.ip4_fragments(sb, O.decode(sb, L.LayerTypeEthernet, ALL, 0, ext=True)), sf)
+
+
+@pytest.mark.gpu
+def test_defragmenter_on_gpu_records():
+    """The same scenarios fed from the GPU hand-off (gpd_ip4_fragments) end to end."""
+    fr = _frames()
+    names = list(fr)
+    parser = _all_parser()
+    got, cnt = _device_fragments(parser, PacketBatch.from_packets([fr[k] for k in names]))
+    assert cnt == 8 and list(got["packet"]) == list(range(8))
+    _defrag_scenarios({k: r for k, r in zip(names, got)})
+    sf = [f for _, f in struct_frames()]
+    got, _ = _device_fragments(parser, PacketBatch.from_packets(sf))
+    _struct_scenarios(got, sf)
