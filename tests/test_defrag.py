@@ -377,3 +377,56 @@ def test_defragmenter_on_gpu_records():
     sf = [f for _, f in struct_frames()]
     got, _ = _device_fragments(parser, PacketBatch.from_packets(sf))
     _struct_scenarios(got, sf)
+
+
+def _rec(off8, length, flags, ident=7, ihl=5, payload_len=None):
+    """A hand-off record for the host defragmenter (packet bytes: 20-B header + payload)."""
+    r = np.zeros((), D.FRAG_DTYPE)
+    r["net_off"], r["ihl"], r["id"], r["frag_offset"], r["length"], r["flags"] = 0, ihl, ident, off8, length, flags
+    r["src"], r["dst"] = [1, 1, 1, 1], [2, 2, 2, 2]
+    r["payload_len"] = length - 4 * ihl if payload_len is None else payload_len
+    r["verdict"] = D.security_verdict(length, ihl, off8)
+    pkt = bytes(4 * ihl) + bytes((off8 * 8 + k) & 0xFF for k in range(int(r["payload_len"])))
+    return r, pkt
+
+
+def test_defragmenter_restates_the_list_rules():
+    """fragmentList.insert / build (defrag.go:216-328) on crafted fragments: out-of-order
+    insertion, a fragment below the highest end but past every stored offset counted and not
+    stored (:222-249), an overlap, a hole (:299-304), and the flush past 8,192 fragments
+    (:117-125), which no admitted sequence reaches."""
+    from gopacket_amd.ip4defrag import NewIPv4Defragmenter
+    # out of order, then complete: payload is the bytes in offset order
+    d = NewIPv4Defragmenter()
+    outs = [d.DefragIPv4WithTimestamp(*_rec(o, 20 + 16, f), 1.0) for o, f in ((4, 0), (0, 1), (2, 1))]
+    assert [o is None for o, _ in outs] == [True, True, False]
+    assert outs[2][0].payload == bytes(range(48)) and outs[2][0].length == 48
+    # counted, not stored: F1 [0, 40) MF, F2 at 16 (< highest 40, past every stored offset)
+    d = NewIPv4Defragmenter()
+    d.DefragIPv4WithTimestamp(*_rec(0, 60, 1), 1.0)
+    d.DefragIPv4WithTimestamp(*_rec(2, 28, 1), 1.0)
+    fl = next(iter(d.ip_flows.values()))
+    assert len(fl.frags) == 1 and fl.highest == 40 and fl.current == 48
+    # an overlap: [0, 24) then [16, 40) (MF clear): build takes bytes 24.. of the second
+    d = NewIPv4Defragmenter()
+    d.DefragIPv4WithTimestamp(*_rec(0, 44, 1), 1.0)
+    out, err = d.DefragIPv4WithTimestamp(*_rec(2, 44, 0), 1.0)
+    assert err is None and out is None  # highest 40 != current 48: not complete
+    # a hole: [8, 16) final with [0, 8) never sent — highest 16, current 8: waits; the
+    # reference only builds when they meet, and a hole found while building is an error
+    d = NewIPv4Defragmenter()
+    assert d.DefragIPv4WithTimestamp(*_rec(1, 28, 0), 1.0) == (None, None)
+    fl = next(iter(d.ip_flows.values()))
+    fl.current = fl.highest  # force the build: the list starts at 8, not 0
+    assert fl.build(fl.frags[0]) == (None, "defrag: building - hole found")
+    # the flush past 8,192 stored fragments cannot trigger: securityChecks admits offsets up to
+    # 8,183 and duplicates are not stored, so a list holds at most 8,184 (Len()+1 <= 8,185)
+    d = NewIPv4Defragmenter()
+    errs = [d.DefragIPv4WithTimestamp(*_rec(k, 28, 1), 1.0)[1] for k in range(8184)]
+    errs += [d.DefragIPv4WithTimestamp(*_rec(k, 28, 1), 1.0)[1] for k in (0, 100, 8183)]
+    assert errs == [None] * 8187 and len(next(iter(d.ip_flows.values())).frags) == 8184
+    # security verdicts come back as the reference's errors
+    r, p = _rec(0, 27, 1)
+    assert d.DefragIPv4WithTimestamp(r, p, 1.0) == (None, "defrag: fragment too small (handcrafted? 7 < 8)")
+    r, p = _rec(8184, 512, 1)
+    assert d.DefragIPv4WithTimestamp(r, p, 1.0) == (None, "defrag: fragment offset too big (handcrafted? 8184 > 8183)")
