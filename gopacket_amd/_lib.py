@@ -11,7 +11,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libgpd.so")
 
-GPD_ABI_VERSION = 5
+GPD_ABI_VERSION = 6
 GPD_OK = 0
 GPD_ERR_INVALID = -1
 

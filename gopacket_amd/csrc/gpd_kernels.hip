@@ -274,9 +274,13 @@ __device__ __forceinline__ Out decode_packet(const S &s, uint32_t caplen, const 
   uint32_t ncount = 0;
   uint64_t codes = 0, ecodes0 = 0, ecodes1 = 0;
   uint32_t stop = 0, klass = GPD_ST_OK;
-  // final (last successful) state of the objects the fused outputs read
+  // final state of the objects the fused outputs read: where their addresses / ports were read
+  // (ip4_off, ip6_off, tcp_poff, udp_off) and their Contents+Payload (ip4_hl, tcp_off/tcp_tot,
+  // udp_off/udp_tot) — the last successful decode of each kind, or what a failing call of that
+  // kind assigned after it (the fail block)
   uint32_t ip4_off = 0, ip4_hl = 0, ip6_off = 0;
-  uint32_t tcp_off = 0, tcp_tot = 0, udp_off = 0, udp_tot = 0;
+  uint32_t tcp_off = 0, tcp_tot = 0, tcp_poff = 0, udp_off = 0, udp_tot = 0;
+  uint32_t err_dec = GPD_NOBJ_NONE, err_wrote = 0;
   uint32_t last_net = 0, last_tp = 0, tp_net = 0;  // net: 1 v4, 2 v6; tp: 1 TCP, 2 UDP
   uint32_t obj_valid = 0;
   gpd_layer_rec rec[EXT ? GPD_NOBJ : 1];
@@ -507,7 +511,7 @@ __device__ __forceinline__ Out decode_packet(const S &s, uint32_t caplen, const 
       }
       if (dec == D_IP4) { ip4_off = c_off; ip4_hl = c_len; last_net = 1; }
       else if (dec == D_IP6) { ip6_off = c_off; last_net = 2; }
-      else if (dec == D_TCP) { tcp_off = c_off; tcp_tot = c_len + p_len; last_tp = 1; tp_net = last_net; }
+      else if (dec == D_TCP) { tcp_off = tcp_poff = c_off; tcp_tot = c_len + p_len; last_tp = 1; tp_net = last_net; }
       else if (dec == D_UDP) { udp_off = c_off; udp_tot = c_len + p_len; last_tp = 2; tp_net = last_net; }
       typ = next;
       off = p_off;
@@ -521,6 +525,54 @@ __device__ __forceinline__ Out decode_packet(const S &s, uint32_t caplen, const 
   goto done;
 fail:
   klass = GPD_ST_DECODE_ERROR;
+  {
+    // What the failing DecodeFromBytes assigned to its reused object before returning
+    // (gpd.h gpd_ext_rec.err_wrote): header fields from `off` (1), and BaseLayer too (2).
+    uint32_t ec_len = 0, ep_off = 0, ep_len = 0;
+    if (dec == D_IP4 && err != GPD_E_IP4_TOO_SHORT) {  // ip4.go:195-210, 235-236
+      err_wrote = 2;
+      ec_len = len; ep_off = off + len;                // Contents = data, Payload nil
+      if (err >= GPD_E_IP4_OPT_LT2) {                  // options: the header split stands
+        uint32_t w[1];
+        load_words(s, off, w);
+        uint32_t length = be16_at(w, 2);
+        if (length == 0) length = len & 0xFFFFu;
+        ec_len = (byte_at(w, 0) & 0x0Fu) * 4u;
+        ep_off = off + ec_len;
+        ep_len = min(len, length) - ec_len;
+      }
+    } else if (dec == D_IP6 && err != GPD_E_IP6_TOO_SHORT) {  // ip6.go:226-235
+      err_wrote = 2;
+      ec_len = 40; ep_off = off + 40; ep_len = len - 40;
+    } else if (dec == D_TCP && err != GPD_E_TCP_TOO_SHORT) {  // tcp.go:234-268
+      err_wrote = err == GPD_E_TCP_DOFF_LT5 ? 1u : 2u;
+      ec_len = len; ep_off = off + len;                // doff overrun: Contents = data
+      if (err >= GPD_E_TCP_OPT_LT2_REM) {              // options: the header split stands
+        ec_len = (s.u8(off + 12) >> 4) * 4u;
+        ep_off = off + ec_len;
+        ep_len = len - ec_len;
+      }
+    } else if (dec == D_UDP && err == GPD_E_UDP_LEN_TOO_SMALL) {  // udp.go:35-41
+      err_wrote = 2;
+      ec_len = 8; ep_off = off + 8;                    // Contents = data[:8], Payload nil
+    } else if (dec == D_LLC && len >= 3) {             // llc.go:35-39
+      err_wrote = 1;
+    }
+    err_dec = dec;
+    if (err_wrote && ((obj_valid >> dec) & 1u)) {  // only kinds in decoded feed the outputs
+      if (dec == D_IP4) { ip4_off = off; ip4_hl = ec_len; }
+      else if (dec == D_IP6) ip6_off = off;
+      else if (dec == D_TCP) {
+        tcp_poff = off;
+        if (err_wrote == 2) { tcp_off = off; tcp_tot = ec_len + ep_len; }
+      } else if (dec == D_UDP) { udp_off = off; udp_tot = 8; }
+    }
+    if (EXT && err_wrote == 2) {
+#pragma unroll
+      for (int k = 0; k < GPD_NOBJ; k++)
+        if ((uint32_t)k == dec) rec[k] = gpd_layer_rec{off, ec_len, ep_off, ep_len};
+    }
+  }
 done:
   if (klass != GPD_ST_DECODE_ERROR && stop != 0)
     klass = (options & GPD_OPT_IGNORE_UNSUPPORTED) ? GPD_ST_OK : GPD_ST_UNSUPPORTED;
@@ -550,14 +602,16 @@ done:
     }
     if (last_tp) {  // tcp/udp.TransportFlow(), tcp.go:331-333, udp.go:123-125
       uint32_t w[1];
-      load_words(s, last_tp == 1 ? tcp_off : udp_off, w);
+      load_words(s, last_tp == 1 ? tcp_poff : udp_off, w);
       uint32_t ept = last_tp == 1 ? 4u : 5u;
       thash = flow_mix(fnv_word(kFnvBasis, w[0], 2), fnv_word(kFnvBasis, w[0] >> 16, 2), ept);
       st |= 1u << 17;
     }
   }
   if (!(options & GPD_OPT_NO_CHECKSUMS)) {
-    if (obj_valid & (1u << D_IP4)) {  // checksum(ip4.Contents), ip4.go:158-179
+    // checksum(ip4.Contents), ip4.go:158-179; an odd-length Contents (a failed Length/IHL
+    // check keeps all of data) makes `checksum` index past the end: a panic, no value
+    if ((obj_valid & (1u << D_IP4)) && !(ip4_hl & 1u)) {
       uint32_t h[5];
       load_words(s, ip4_off, h);
       h[2] &= 0x0000FFFFu;  // bytes 10-11 read as zero
@@ -598,7 +652,7 @@ done:
   o.tp_hash = thash;
   o.csum = cs;
   o.hoff = hdr_word(last_net != 0, last_net == 1 ? ip4_off : ip6_off, last_tp != 0,
-                    last_tp == 1 ? tcp_off : udp_off);
+                    last_tp == 1 ? tcp_poff : udp_off);
   if (EXT) {
     gpd_ext_rec e;
     e.layer_codes[0] = ecodes0;
@@ -606,11 +660,13 @@ done:
     e.err_arg0 = klass == GPD_ST_DECODE_ERROR ? a0 : 0;
     e.err_arg1 = klass == GPD_ST_DECODE_ERROR ? a1 : 0;
     e.obj_valid = (uint16_t)obj_valid;
-    e.pad0 = 0;
-    e.pad1 = 0;
+    e.err_obj = (uint8_t)err_dec;  // Dec order == enum gpd_obj order
+    e.err_wrote = (uint8_t)err_wrote;
+    e.err_off = klass == GPD_ST_DECODE_ERROR ? off : 0;
 #pragma unroll
     for (int k = 0; k < GPD_NOBJ; k++)
-      e.obj[k] = (obj_valid >> k) & 1u ? rec[k] : gpd_layer_rec{0, 0, 0, 0};
+      e.obj[k] = ((obj_valid >> k) & 1u) || ((uint32_t)k == err_dec && err_wrote == 2)
+                     ? rec[k] : gpd_layer_rec{0, 0, 0, 0};
     *ext = e;
   }
   return o;
@@ -2011,8 +2067,8 @@ static hipError_t launch_s(const KParams &P, hipStream_t stream, int num_cus) {
 // candidate bit per packet), their exclusive scan, the candidates' packet indices in order, and
 // one record per candidate.
 
-// Can packet i's IPv4 object (the last IPv4 in decoded) be a fragment?  From the result words
-// first: a fragmented IPv4 layer ends the decode (ip4.go:281-286, its next layer is
+// Can packet i's IPv4 object (as the call leaves it: the last IPv4 in decoded, or a later IPv4
+// call that failed after assigning its fields) be a fragment?  From the result words first: a fragmented IPv4 layer ends the decode (ip4.go:281-286, its next layer is
 // gopacket.Fragment, which decodes nothing further), so decoded ends [.., IPv4, Fragment], or
 // [.., IPv4] with Fragment unregistered (stop type 3) or the payload empty (stop 0).  Then the
 // flags/offset word of the header (ip4.go:193,200-201), which also rules out DF (:164-166).
@@ -2028,7 +2084,10 @@ __device__ __forceinline__ bool frag_candidate(const KParams &P, uint32_t i) {
   }
   if (GPD_STATUS_NET_EPT(st) != 1u) return false;  // the last network layer is not IPv4
   const uint32_t nl = GPD_STATUS_NLAYERS(st);
-  if (nl <= GPD_CORE_MAX_LAYERS && !GPD_STATUS_SATURATED(st)) {
+  // After a decode error the ip4 object may hold a later, failed IPv4 header (ip4.go:195-210
+  // assign its fields before the Length/IHL checks) wherever decoded ends: the header decides.
+  if (GPD_STATUS_CLASS(st) != GPD_ST_DECODE_ERROR && nl <= GPD_CORE_MAX_LAYERS &&
+      !GPD_STATUS_SATURATED(st)) {
     const uint32_t last = GPD_LAYERS_CODE(lw, nl - 1), stop = GPD_LAYERS_STOP(lw);
     const bool maybe = (last == GPD_C_FRAGMENT && nl >= 2 && GPD_LAYERS_CODE(lw, nl - 2) == GPD_C_IPV4) ||
                        (last == GPD_C_IPV4 && (stop == 0 || stop == GPD_LT_FRAGMENT));

@@ -27,7 +27,7 @@ RECORD_DTYPE = np.dtype([("status", "<u4"), ("csum", "<u4"), ("layers", "<u8"), 
 assert RECORD_DTYPE.itemsize == 32
 
 EXT_DTYPE = np.dtype([("layer_codes", "<u8", (2,)), ("err_arg0", "<u4"), ("err_arg1", "<u4"),
-                      ("obj_valid", "<u2"), ("pad0", "<u2"), ("pad1", "<u4"),
+                      ("obj_valid", "<u2"), ("err_obj", "u1"), ("err_wrote", "u1"), ("err_off", "<u4"),
                       ("obj", LAYER_REC_DTYPE, (12,))])
 assert EXT_DTYPE.itemsize == 224
 

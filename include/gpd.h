@@ -46,9 +46,10 @@
 extern "C" {
 #endif
 
-#define GPD_ABI_VERSION 5  /* 2: ICMPv4 + LLC, 12 objects, 224-B ext; 3: gpd_result.hdr_off;
+#define GPD_ABI_VERSION 6  /* 2: ICMPv4 + LLC, 12 objects, 224-B ext; 3: gpd_result.hdr_off;
                               4: gpd_ctx_set_tuning; 5: gpd_tuning.header_once,
-                              gpd_tuning.device_walk, gpd_result.records */
+                              gpd_tuning.device_walk, gpd_result.records; 6: outputs follow the
+                              objects as a failing call leaves them; ext err_obj/err_wrote/err_off */
 
 /* ---- gopacket LayerType numbers (layertypes.go:14-154, decode.go:105-116) ---- */
 #define GPD_LT_ZERO            0
@@ -108,13 +109,18 @@ extern "C" {
  *  [15]    reserved (0)
  *  [16]    net_hash valid   (an IPv4/IPv6 layer is in decoded)
  *  [17]    tp_hash valid    (a TCP/UDP layer is in decoded)
- *  [18]    IPv4 header checksum valid (IPv4 in decoded)
+ *  [18]    IPv4 header checksum valid (IPv4 in decoded, and len(ip4.Contents) even: after a
+ *          failed Length/IHL check Contents is the whole remaining data, ip4.go:210, and an odd
+ *          length makes `checksum` index past the end, ip4.go:165-167 — a panic in Go)
  *  [19]    L4 checksum valid (TCP/UDP in decoded, preceded by IPv4/IPv6)
  *  [23:20] EndpointType of NetworkFlow(): of the last IPv4/IPv6 in decoded (1 IPv4, 2 IPv6,
  *          0 none; layers/endpoints.go:20-23), whether or not hashes are computed
  *  [27:24] EndpointType of TransportFlow(): of the last TCP/UDP (4 TCP, 5 UDP, 0 none;
  *          layers/endpoints.go:29-32)
- *  [31:28] reserved (0)                                                          */
+ *  [31:28] reserved (0)
+ * The hashes and checksums read each layer object as the call leaves it, which is not always
+ * its last successful decode: a later DecodeFromBytes of the same kind that fails may already
+ * have assigned addresses / ports / BaseLayer (see gpd_ext_rec.err_wrote).                */
 #define GPD_ST_OK            0u
 #define GPD_ST_UNSUPPORTED   1u
 #define GPD_ST_DECODE_ERROR  2u
@@ -210,9 +216,14 @@ enum gpd_obj {
   GPD_NOBJ = 12
 };
 
-/* BaseLayer of one object after its last successful DecodeFromBytes in this packet:
+#define GPD_NOBJ_NONE 0xFFu
+
+/* BaseLayer of one object as the call leaves it (offsets relative to the packet):
  * Contents = pkt[contents_off : contents_off+contents_len],
- * Payload  = pkt[payload_off  : payload_off+payload_len]  (offsets relative to the packet). */
+ * Payload  = pkt[payload_off  : payload_off+payload_len]; a nil Payload is length 0 at the end
+ * of Contents.  The parser reuses one object per kind (layers_decoder.go:61-78), so this is the
+ * object's last successful DecodeFromBytes in the packet — unless a later call on the same
+ * object failed after assigning BaseLayer (err_wrote == 2 below), which then wins. */
 typedef struct gpd_layer_rec {
   uint32_t contents_off, contents_len, payload_off, payload_len;
 } gpd_layer_rec;
@@ -223,9 +234,22 @@ typedef struct gpd_ext_rec {
   uint64_t layer_codes[2];  /* decoded[0..31] as 4-bit codes, decoded[i] at bit 4*(i%16) of word i/16 */
   uint32_t err_arg0;        /* first %d/%v argument of the error text (see enum gpd_err) */
   uint32_t err_arg1;        /* second argument, if any */
-  uint16_t obj_valid;       /* bit k: object k decoded successfully at least once */
-  uint16_t pad0;
-  uint32_t pad1;
+  uint16_t obj_valid;       /* bit k: object k decoded successfully at least once (its kind is
+                               in decoded); obj[k] is then its BaseLayer as the call leaves it */
+  uint8_t  err_obj;         /* decode error: object (enum gpd_obj) whose DecodeFromBytes failed;
+                               GPD_NOBJ_NONE otherwise */
+  uint8_t  err_wrote;       /* what that failing call assigned before it returned:
+                               0 nothing (the length checks come first);
+                               1 header fields read from pkt[err_off:] (TCP doff < 5: ports ..
+                                 Urgent, tcp.go:234-259; LLC: DSAP .. Control, llc.go:35-39),
+                                 BaseLayer unchanged;
+                               2 header fields from pkt[err_off:] and BaseLayer, recorded in
+                                 obj[err_obj] (IPv4 after len >= 20: Contents = data, Payload nil,
+                                 ip4.go:195-210, or the header split for option errors :235-236;
+                                 IPv6 after len >= 40, ip6.go:226-235; TCP doff overrun
+                                 (Contents = data, tcp.go:264-268) and option errors; UDP
+                                 "too small", Contents = data[:8], udp.go:35-41) */
+  uint32_t err_off;         /* offset of the data the failing DecodeFromBytes was given */
   gpd_layer_rec obj[GPD_NOBJ];
 } gpd_ext_rec;
 
@@ -260,10 +284,11 @@ typedef struct gpd_batch {
 } gpd_batch;
 
 /* ---- header offsets word (uint32): where the flows' layers sit in the packet ----
- *  [15:0]  offset (from the packet start) of the network layer NetworkFlow() reads: the
- *          last IPv4/IPv6 in decoded (ip4/ip6.Contents[0]); 0xFFFF if none
- *  [31:16] offset of the transport layer TransportFlow() reads: the last TCP/UDP in
- *          decoded; 0xFFFF if none
+ *  [15:0]  offset (from the packet start) of the header whose SrcIP/DstIP NetworkFlow()
+ *          reads: the object of the kind of the last IPv4/IPv6 in decoded, as the call leaves
+ *          it (a later failing call of that kind may have re-assigned them); 0xFFFF if none
+ *  [31:16] the same for the ports TransportFlow() reads (the last TCP/UDP in decoded);
+ *          0xFFFF if none
  * Offsets >= 0xFFFF saturate to 0xFFFF.  With these a caller fills the layer structs (or
  * builds the [2]Flow key tcpassembly uses) straight from the packet bytes, zero copy. */
 #define GPD_HDR_NET(h) ((uint32_t)((h) & 0xFFFFu))

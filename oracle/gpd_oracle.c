@@ -25,6 +25,11 @@ typedef struct {
   uint32_t err, a0, a1;         /* the error returned by DecodeFromBytes */
   sl contents, payload;         /* BaseLayer set by the current DecodeFromBytes */
   uint32_t next;                /* NextLayerType() of the current layer */
+  /* What a failing DecodeFromBytes already wrote into its reused object before it returned
+   * (the parser keeps one object per kind, layers_decoder.go:61-78): 0 nothing, 1 header
+   * fields read from data (addresses, ports...), 2 those fields and BaseLayer (contents /
+   * payload above, a nil Payload as length 0 at the end of Contents). */
+  int wrote;
 } st;
 
 static uint32_t be16(const uint8_t *p) { return ((uint32_t)p[0] << 8) | p[1]; }
@@ -79,6 +84,11 @@ static int dec_dot1q(st *s, sl d) {
 static int dec_ipv4(st *s, sl d) {
   const uint8_t *p = s->pkt + d.off;
   if (d.len < 20) { s->truncated = 1; return fail(s, GPD_E_IP4_TOO_SHORT, d.len, 0); }
+  /* ip4.go:195-210: every header field, then BaseLayer{Contents: data} (Payload nil), are set
+   * before the Length/IHL checks; a later error leaves them so */
+  s->wrote = 2;
+  s->contents = d;
+  s->payload = (sl){d.off + d.len, 0};
   uint32_t flagsfrags = be16(p + 6);
   uint32_t ihl = p[0] & 0x0F;
   uint32_t length = be16(p + 2);
@@ -133,6 +143,8 @@ static int dec_ipv6(st *s, sl d) {
   if (d.len < 40) { s->truncated = 1; return fail(s, GPD_E_IP6_TOO_SHORT, d.len, 0); }
   uint32_t length = be16(p + 4);
   uint32_t nh = p[6];
+  /* ip6.go:226-235: fields and BaseLayer{data[:40], data[40:]} before the HBH / length errors */
+  s->wrote = 2;
   s->contents = (sl){d.off, 40};
   s->payload = (sl){d.off + 40, d.len - 40};
   int have_hbh = 0;
@@ -206,9 +218,16 @@ static int dec_tcp(st *s, sl d) {
   if (d.len < 20) { s->truncated = 1; return fail(s, GPD_E_TCP_TOO_SHORT, d.len, 0); }
   uint32_t sport = be16(p), dport = be16(p + 2);
   uint32_t doff = p[12] >> 4;
+  s->wrote = 1;  /* tcp.go:234-259: ports .. Urgent; BaseLayer untouched by the doff error */
   if (doff < 5) return fail(s, GPD_E_TCP_DOFF_LT5, doff, 0);
   uint32_t ds = doff * 4;
-  if (ds > d.len) { s->truncated = 1; return fail(s, GPD_E_TCP_DOFF_GT_LEN, 0, 0); }
+  s->wrote = 2;
+  if (ds > d.len) {  /* tcp.go:264-268: Payload = nil, Contents = data */
+    s->contents = d;
+    s->payload = (sl){d.off + d.len, 0};
+    s->truncated = 1;
+    return fail(s, GPD_E_TCP_DOFF_GT_LEN, 0, 0);
+  }
   s->contents = (sl){d.off, ds};
   s->payload = (sl){d.off + ds, d.len - ds};
   for (uint32_t o = 20; o < ds;) {                      /* OPTIONS loop, tcp.go:274-300 */
@@ -236,7 +255,11 @@ static int dec_udp(st *s, sl d) {
   const uint8_t *p = s->pkt + d.off;
   if (d.len < 8) { s->truncated = 1; return fail(s, GPD_E_UDP_TOO_SHORT, d.len, 0); }
   uint32_t sport = be16(p), dport = be16(p + 2), length = be16(p + 4);
+  /* udp.go:35-41: ports, Length, Checksum, BaseLayer{Contents: data[:8]} (Payload nil) before
+   * the "too small" error */
+  s->wrote = 2;
   s->contents = (sl){d.off, 8};
+  s->payload = (sl){d.off + 8, 0};
   if (length >= 8) {
     uint32_t hlen = length;
     if (hlen > d.len) { s->truncated = 1; hlen = d.len; }
@@ -274,6 +297,7 @@ static int dec_icmp4(st *s, sl d) {
 static int dec_llc(st *s, sl d) {
   const uint8_t *p = s->pkt + d.off;
   if (d.len < 3) return fail(s, GPD_E_LLC_TOO_SMALL, 0, 0);
+  s->wrote = 1;  /* llc.go:35-39: DSAP .. Control before the second length check */
   uint32_t dsap = p[0] & 0xFE, ssap = p[1] & 0xFE, control = p[2];
   uint32_t hl = 3;
   if ((control & 0x1) == 0 || (control & 0x3) == 0x1) {
@@ -426,9 +450,13 @@ void gpo_decode_packet(const uint8_t *pkt, uint32_t caplen, uint32_t first, uint
   memset(&s, 0, sizeof s);
   s.pkt = pkt;
   s.t = t;
-  int obj_ok[GPD_NOBJ] = {0};
-  gpd_layer_rec obj[GPD_NOBJ];
+  int obj_ok[GPD_NOBJ] = {0};     /* the kind is in decoded (one successful call at least) */
+  gpd_layer_rec obj[GPD_NOBJ];    /* each object's BaseLayer as the call leaves it */
+  uint32_t fbase[GPD_NOBJ];       /* where its header fields (addresses, ports) were read */
   memset(obj, 0, sizeof obj);
+  memset(fbase, 0, sizeof fbase);
+  int err_obj = -1, err_wrote = 0;
+  uint32_t err_off = 0;
   uint32_t ncount = 0;
   uint64_t core_codes = 0, ext_codes[2] = {0, 0};
   int last_net = -1, last_tp = -1, tp_net = -1; /* object ids */
@@ -443,6 +471,7 @@ void gpo_decode_packet(const uint8_t *pkt, uint32_t caplen, uint32_t first, uint
     sl data = {0, caplen};
     for (;;) {
       int rc;
+      s.wrote = 0;
       switch (dec) {
         case D_ETH: rc = dec_ethernet(&s, data); break;
         case D_DOT1Q: rc = dec_dot1q(&s, data); break;
@@ -456,7 +485,22 @@ void gpo_decode_packet(const uint8_t *pkt, uint32_t caplen, uint32_t first, uint
         case D_LLC: rc = dec_llc(&s, data); break;
         default: rc = dec_rest(&s, data); break;
       }
-      if (rc) { klass = GPD_ST_DECODE_ERROR; break; }
+      if (rc) {
+        /* The failing call's object keeps what it wrote before returning (ip4.go:195-210,
+         * ip6.go:226-235, tcp.go:234-268, udp.go:35-41, llc.go:35-39) */
+        klass = GPD_ST_DECODE_ERROR;
+        err_obj = obj_of_dec[dec];
+        err_off = data.off;
+        err_wrote = s.wrote;
+        if (s.wrote >= 1) fbase[err_obj] = data.off;
+        if (s.wrote == 2) {
+          obj[err_obj].contents_off = s.contents.off;
+          obj[err_obj].contents_len = s.contents.len;
+          obj[err_obj].payload_off = s.payload.off;
+          obj[err_obj].payload_len = s.payload.len;
+        }
+        break;
+      }
       /* *decoded = append(*decoded, typ) */
       uint32_t code = code_of(typ);
       if (ncount < GPD_CORE_MAX_LAYERS) core_codes |= (uint64_t)code << (16 + 4 * ncount);
@@ -468,6 +512,7 @@ void gpo_decode_packet(const uint8_t *pkt, uint32_t caplen, uint32_t first, uint
       obj[o].contents_len = s.contents.len;
       obj[o].payload_off = s.payload.off;
       obj[o].payload_len = s.payload.len;
+      fbase[o] = data.off;
       if (o == GPD_OBJ_IPV4 || o == GPD_OBJ_IPV6) last_net = o;
       if (o == GPD_OBJ_TCP || o == GPD_OBJ_UDP) { last_tp = o; tp_net = last_net; }
       typ = s.next;
@@ -492,21 +537,24 @@ void gpo_decode_packet(const uint8_t *pkt, uint32_t caplen, uint32_t first, uint
   if (last_net >= 0) status |= (last_net == GPD_OBJ_IPV4 ? 1u : 2u) << 20;
   if (last_tp >= 0) status |= (last_tp == GPD_OBJ_TCP ? 4u : 5u) << 24;
   if (!(options & GPD_OPT_NO_FLOW_HASH)) {
-    if (last_net >= 0) {
-      const uint8_t *c = pkt + obj[last_net].contents_off;
+    if (last_net >= 0) {  /* ip4/ip6.NetworkFlow() over SrcIP/DstIP as last written */
+      const uint8_t *c = pkt + fbase[last_net];
       if (last_net == GPD_OBJ_IPV4) nh = gpo_flow_fasthash(1, c + 12, 4, c + 16, 4);
       else nh = gpo_flow_fasthash(2, c + 8, 16, c + 24, 16);
       status |= 1u << 16;
     }
-    if (last_tp >= 0) {
-      const uint8_t *c = pkt + obj[last_tp].contents_off;
+    if (last_tp >= 0) {  /* tcp/udp.TransportFlow() over sPort/dPort as last written */
+      const uint8_t *c = pkt + fbase[last_tp];
       uint32_t ept = last_tp == GPD_OBJ_TCP ? 4 : 5;
       th = gpo_flow_fasthash(ept, c, 2, c + 2, 2);
       status |= 1u << 17;
     }
   }
   if (!(options & GPD_OPT_NO_CHECKSUMS)) {
-    if (obj_ok[GPD_OBJ_IPV4]) {
+    /* checksum(ip4.Contents): after a failed Length/IHL check Contents is all of that call's
+     * data (ip4.go:210); an odd length makes `checksum` index past the end (ip4.go:165-167),
+     * a Go panic, so that case reports no value (bit 18 clear) */
+    if (obj_ok[GPD_OBJ_IPV4] && (obj[GPD_OBJ_IPV4].contents_len & 1u) == 0) {
       csum |= gpo_ip4_header_checksum(pkt + obj[GPD_OBJ_IPV4].contents_off,
                                       obj[GPD_OBJ_IPV4].contents_len);
       status |= 1u << 18;
@@ -515,7 +563,7 @@ void gpo_decode_packet(const uint8_t *pkt, uint32_t caplen, uint32_t first, uint
       /* tcp.SetNetworkLayerForChecksum(net); tcp.ComputeChecksum() (tcp.go:193-195,
        * tcpip.go:75-88): append(Contents, Payload...) with the pseudo-header of `net` */
       const gpd_layer_rec *r = &obj[last_tp];
-      const uint8_t *nc = pkt + obj[tp_net].contents_off;
+      const uint8_t *nc = pkt + fbase[tp_net];
       uint32_t ps = tp_net == GPD_OBJ_IPV4 ? gpo_pseudo_v4(nc + 12, nc + 16)
                                           : gpo_pseudo_v6(nc + 8, nc + 24);
       uint32_t length = r->contents_len + r->payload_len;
@@ -533,18 +581,26 @@ void gpo_decode_packet(const uint8_t *pkt, uint32_t caplen, uint32_t first, uint
   if (tp_hash_out) *tp_hash_out = th;
   if (csum_out) *csum_out = csum;
   if (hdr_off_out) { /* gpd.h header offsets word: the objects NetworkFlow/TransportFlow read */
-    uint32_t a = last_net >= 0 ? obj[last_net].contents_off : 0xFFFFu;
-    uint32_t b = last_tp >= 0 ? obj[last_tp].contents_off : 0xFFFFu;
+    uint32_t a = last_net >= 0 ? fbase[last_net] : 0xFFFFu;
+    uint32_t b = last_tp >= 0 ? fbase[last_tp] : 0xFFFFu;
     *hdr_off_out = (a < 0xFFFFu ? a : 0xFFFFu) | ((b < 0xFFFFu ? b : 0xFFFFu) << 16);
   }
   if (ext) {
     memset(ext, 0, sizeof *ext);
     ext->layer_codes[0] = ext_codes[0];
     ext->layer_codes[1] = ext_codes[1];
-    if (klass == GPD_ST_DECODE_ERROR) { ext->err_arg0 = s.a0; ext->err_arg1 = s.a1; }
+    ext->err_obj = GPD_NOBJ_NONE;
+    if (klass == GPD_ST_DECODE_ERROR) {
+      ext->err_arg0 = s.a0;
+      ext->err_arg1 = s.a1;
+      ext->err_obj = (uint8_t)err_obj;
+      ext->err_wrote = (uint8_t)err_wrote;
+      ext->err_off = err_off;
+    }
     uint32_t valid = 0;
     for (int o = 0; o < GPD_NOBJ; o++) {
-      if (obj_ok[o]) { valid |= 1u << o; ext->obj[o] = obj[o]; }
+      if (obj_ok[o]) valid |= 1u << o;
+      if (obj_ok[o] || (o == err_obj && err_wrote == 2)) ext->obj[o] = obj[o];
     }
     ext->obj_valid = (uint16_t)valid;
   }
