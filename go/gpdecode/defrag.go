@@ -45,13 +45,20 @@ type Fragment struct {
 	Verdict     uint8
 }
 
-// Layer rebuilds the DecodingLayerParser's IPv4 object for the fragment: DecodeFromBytes over
-// exactly the bytes the parser gave it (Contents + Payload), so Length, Payload and the
-// truncation flag come out as the batch decode left them.
-func (f *Fragment) Layer(b *PacketBatch, ip *layers.IPv4) error {
+// Layer rebuilds the DecodingLayerParser's IPv4 object for the fragment in a NEW layer over a
+// COPY of its bytes: DecodeFromBytes over exactly the bytes the parser gave it (Contents +
+// Payload), so Length, Payload and the truncation flag come out as the batch decode left them.
+// A fresh object per fragment matters: IPv4Defragmenter keeps the *layers.IPv4 it is given in
+// its pending list until the datagram completes (ip4defrag/defrag.go:221,245), and the copy
+// keeps pending fragments valid when the batch buffer is reused for the next batch.
+// (A packet whose IPv4 decode FAILED after assigning the header fields — the parser's object
+// then holds that rejected header, ip4.go:195-210 — comes back with the same decode error.)
+func (f *Fragment) Layer(b *PacketBatch) (*layers.IPv4, error) {
 	pkt := b.Data[b.Offset[f.Packet] : b.Offset[f.Packet]+b.CapLen[f.Packet]]
 	end := f.NetOff + 4*uint32(f.IHL) + f.PayloadLen
-	return ip.DecodeFromBytes(pkt[f.NetOff:end], gopacket.NilDecodeFeedback)
+	buf := append([]byte(nil), pkt[f.NetOff:end]...)
+	ip := new(layers.IPv4)
+	return ip, ip.DecodeFromBytes(buf, gopacket.NilDecodeFeedback)
 }
 
 // Err is the error DefragIPv4 returns for the fragment without filing it (nil for FragInsert
@@ -75,8 +82,9 @@ func (f *Fragment) Err() error {
 //	for i := range frags {
 //	    f := &frags[i]
 //	    if err := f.Err(); err != nil { ...; continue }      // securityChecks
-//	    f.Layer(&b, &ip4)
-//	    whole, _ := defragger.DefragIPv4WithTimestamp(&ip4, ts[f.Packet])
+//	    ip4, err := f.Layer(&b)                               // its own object, its own bytes
+//	    if err != nil { ...; continue }
+//	    whole, _ := defragger.DefragIPv4WithTimestamp(ip4, ts[f.Packet])
 //	}
 //
 // Every other packet skips the defragmenter.

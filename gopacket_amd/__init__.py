@@ -4,8 +4,9 @@ The product path is libgpd.so (HIP kernels for gfx950 behind the C-ABI in
 include/gpd.h); this package is the host-side mirror of gopacket's parser API
 (parser.py), its dispatch tables (layers.py), batch layout (batch.py), result
 reading (results.py), input formats (pcap.py, afpacket.py, synth.py), the flow table
-(flows.py), the IPv4 fragment hand-off to ip4defrag (defrag.py) and the host-side
-reassembly over it (ip4defrag.py).
+(flows.py) and the IPv4 fragment hand-off to ip4defrag (defrag.py).  (The stateful
+reassembly over that hand-off is restated only as a test checker, oracle/ip4defrag_ref.py:
+ip4defrag itself is out of scope.)
 """
 from . import layers
 from .layers import *  # noqa: F401,F403  LayerType constants, Register*PortLayerType

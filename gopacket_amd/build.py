@@ -29,7 +29,7 @@ SOURCES = [os.path.join(CSRC, "gpd_kernels.hip"), os.path.join(CSRC, "gpd_runtim
            os.path.join(CSRC, "gpd_afpacket.cpp")]
 HEADERS = [os.path.join(CSRC, "gpd_internal.h"), os.path.join(ROOT, "include", "gpd.h"),
            os.path.join(ROOT, "include", "gpd_pcap.h"), os.path.join(ROOT, "include", "gpd_flow.h"),
-           os.path.join(ROOT, "include", "gpd_afpacket.h")]
+           os.path.join(ROOT, "include", "gpd_afpacket.h"), os.path.join(ROOT, "include", "gpd_defrag.h")]
 
 
 def _stale(target, deps):

@@ -68,7 +68,12 @@ def IPv4Fragments(parser: DecodingLayerParser, dbatch: DeviceBatch, dres: Device
     return out, int(cnt.value)
 
 
-def fragments_to_host(out, count: int) -> np.ndarray:
-    """FRAG_DTYPE[count] copy of IPv4Fragments' records (at most what `out` holds)."""
+def fragments_to_host(out, count: int, allow_partial: bool = False) -> np.ndarray:
+    """FRAG_DTYPE[count] copy of IPv4Fragments' records.  When the batch had more fragments
+    than `out` holds (IPv4Fragments' max_out), raises unless allow_partial: a defragmenter fed
+    only the first records would report holes or never complete the datagrams."""
     k = min(count, out.numel() // FRAG_DTYPE.itemsize)
+    if k < count and not allow_partial:
+        raise ValueError(f"fragments_to_host: {count} fragments, `out` holds {k}; "
+                         f"call IPv4Fragments with a larger max_out")
     return out[:k * FRAG_DTYPE.itemsize].cpu().numpy().view(FRAG_DTYPE).copy()

@@ -3,6 +3,7 @@
   config 2  make_udp64(n)   64 B Eth/IPv4/UDP, seed 0x5EED0002
   config 3  make_imix(n)    IMIX 64/576/1500 (7:4:1) Eth/Dot1Q/IPv4/TCP, seed 0x5EED0003
   config 4  make_vxlan(n)   128 B Eth/IPv4/UDP:4789/VXLAN/Eth/IPv4/TCP, seed 0x5EED0004
+  (north star) make_tcp64(n) 64 B Eth/IPv4/TCP, seed 0x5EED0008
 
 Random fields come from a vectorised splitmix64 stream; ports avoid every key of
 the reference's port tables (layers/ports.go:62-122) so the transport's next layer
@@ -122,17 +123,46 @@ def _udp64_rows(a: np.ndarray, seed: int, base: int, free: np.ndarray) -> None:
     _corrupt(a, bad, 24)  # IPv4 header checksum byte
 
 
-def make_udp64(n: int, seed: int = 0x5EED0002, chunk: int = 1 << 20) -> PacketBatch:
+def _parallel(jobs) -> None:
+    """Run independent chunk jobs on a thread pool: numpy's kernels release the GIL, and every
+    chunk's bytes depend only on (seed, stream, packet index), so the result is the same bytes
+    whatever the order."""
+    import os
+    from concurrent.futures import ThreadPoolExecutor
+    try:
+        nt = len(os.sched_getaffinity(0))
+    except AttributeError:
+        nt = os.cpu_count() or 1
+    nt = max(1, min(16, nt, len(jobs)))
+    if nt == 1:
+        for j in jobs:
+            j()
+        return
+    with ThreadPoolExecutor(nt) as ex:
+        for f in [ex.submit(j) for j in jobs]:
+            f.result()
+
+
+def _fixed_rows(n: int, size: int, fill, chunk: int) -> PacketBatch:
+    """n frames of `size` bytes back to back; fill(rows, base) writes rows base .. base+len."""
+    data = np.zeros(n * size + PAD, dtype=np.uint8)
+    rows = data[: n * size].reshape(n, size)
+
+    def job(c0):
+        def run():
+            a = np.zeros((min(chunk, n - c0), size), dtype=np.uint8)
+            fill(a, c0)
+            rows[c0:c0 + a.shape[0]] = a
+        return run
+    _parallel([job(c0) for c0 in range(0, n, chunk)])
+    return PacketBatch(data, n * size, (np.arange(n, dtype=np.uint64) * size).astype(np.uint32),
+                       np.full(n, size, dtype=np.uint32))
+
+
+def make_udp64(n: int, seed: int = 0x5EED0002, chunk: int = 1 << 18) -> PacketBatch:
     """Config 2: 64 B Eth/IPv4/UDP (IHL 5, Length 50, UDP Length 30)."""
-    data = np.zeros(n * 64 + PAD, dtype=np.uint8)
-    rows = data[: n * 64].reshape(n, 64)
     free = _free_ports(TABLES.udp_port)
-    for c0 in range(0, n, chunk):
-        a = np.zeros((min(chunk, n - c0), 64), dtype=np.uint8)
-        _udp64_rows(a, seed, c0, free)
-        rows[c0:c0 + a.shape[0]] = a
-    return PacketBatch(data, n * 64, (np.arange(n, dtype=np.uint64) * 64).astype(np.uint32),
-                       np.full(n, 64, dtype=np.uint32))
+    return _fixed_rows(n, 64, lambda a, base: _udp64_rows(a, seed, base, free), chunk)
 
 
 _native = None
@@ -174,10 +204,10 @@ IMIX_WEIGHTS = (7, 4, 1)
 
 
 def _tcp_frames(n: int, size: int, r: list, opts: np.ndarray, vlan: bool, free: np.ndarray,
-                bad: np.ndarray, seed: int, stream: int) -> np.ndarray:
+                bad: np.ndarray, seed: int, stream: int, base: int = 0) -> np.ndarray:
     """n Eth(/Dot1Q)/IPv4/TCP frames of `size` bytes; rows in `opts` carry NOP,NOP,TS."""
     a = np.zeros((n, size), dtype=np.uint8)
-    a[:, 0:12] = _rand_bytes(seed, stream, n, 12) & 0xFE
+    a[:, 0:12] = _rand_bytes(seed, stream, n, 12, base) & 0xFE
     c = 12
     if vlan:
         _be16(a, 12, np.full(n, 0x8100))
@@ -200,7 +230,7 @@ def _tcp_frames(n: int, size: int, r: list, opts: np.ndarray, vlan: bool, free: 
     a[:, l4 + 13] = 0x10 | (((r[2] >> np.uint64(24)) & np.uint64(1)).astype(np.uint8) << 3)  # ACK(+PSH)
     _be16(a, l4 + 14, ((r[2] >> np.uint64(32)) & np.uint64(0xFFFF)).astype(np.int64))
     if seg > 20:
-        body = _rand_bytes(seed, stream + 1, n, seg - 20)
+        body = _rand_bytes(seed, stream + 1, n, seg - 20, base)
         a[:, l4 + 20:] = body
     if len(opts):
         a[opts, l4 + 12] = 0x80
@@ -237,10 +267,8 @@ def make_imix(n: int, seed: int = 0x5EED0003, vlan: bool = True, align: int = 16
     bad_all = (gidx % 64) == 63
     ropt = splitmix64(seed, n, 98)
     opt_all = (cls > 0) & ((ropt % np.uint64(10)) < np.uint64(3))
-    for k, size in enumerate(IMIX_SIZES):
-        rows_all = np.nonzero(cls == k)[0]
-        for c0 in range(0, len(rows_all), chunk):
-            rows = rows_all[c0:c0 + chunk]
+    def job(k, size, rows, c0):
+        def run():
             m = len(rows)
             r = [splitmix64(seed + c0, m, 16 * k + j) for j in range(6)]
             opts = np.nonzero(opt_all[rows])[0]
@@ -248,16 +276,19 @@ def make_imix(n: int, seed: int = 0x5EED0003, vlan: bool = True, align: int = 16
             frames = _tcp_frames(m, size, r, opts, vlan, free, bad, seed + c0, 200 + 2 * k)
             idx = offs[rows][:, None] + np.arange(size)[None, :]
             data[idx.reshape(-1)] = frames.reshape(-1)
+        return run
+    jobs = []
+    for k, size in enumerate(IMIX_SIZES):
+        rows_all = np.nonzero(cls == k)[0]
+        jobs += [job(k, size, rows_all[c0:c0 + chunk], c0) for c0 in range(0, len(rows_all), chunk)]
+    _parallel(jobs)
     return PacketBatch(data, total, offs.astype(np.uint32), sizes.astype(np.uint32))
 
 
-def make_vxlan(n: int, seed: int = 0x5EED0004) -> PacketBatch:
-    """Config 4: 128 B Eth/IPv4/UDP(4789)/VXLAN/Eth/IPv4/TCP (104 B of headers + 24 B payload)."""
-    a = np.zeros((n, 128), dtype=np.uint8)
-    r = [splitmix64(seed, n, k) for k in range(10)]
-    free_u = _free_ports(TABLES.udp_port)
-    free_t = _free_ports(TABLES.tcp_port)
-    a[:, 0:12] = _rand_bytes(seed, 100, n, 12) & 0xFE
+def _vxlan_rows(a: np.ndarray, seed: int, base: int, free_u: np.ndarray, free_t: np.ndarray) -> None:
+    n = a.shape[0]
+    r = [splitmix64(seed, n, k, base) for k in range(10)]
+    a[:, 0:12] = _rand_bytes(seed, 100, n, 12, base) & 0xFE
     _be16(a, 12, np.full(n, 0x0800))
     _ip4_header(a, 14, np.full(n, 114), (r[1] & np.uint64(0xFFFF)).astype(np.int64),
                 np.full(n, 64, np.uint8), 17, (r[2] & np.uint64(0xFFFFFFFF)),
@@ -267,7 +298,7 @@ def make_vxlan(n: int, seed: int = 0x5EED0004) -> PacketBatch:
     _be16(a, 38, np.full(n, 94))
     a[:, 42] = 0x08  # VXLAN I flag
     _be32(a, 46, (r[4] & np.uint64(0xFFFFFF)) << np.uint64(8))
-    a[:, 50:62] = _rand_bytes(seed, 101, n, 12) & 0xFE
+    a[:, 50:62] = _rand_bytes(seed, 101, n, 12, base) & 0xFE
     _be16(a, 62, np.full(n, 0x0800))
     ttl = ((r[6] >> np.uint64(16)) & np.uint64(0xFF)).astype(np.uint8) | 1
     _ip4_header(a, 64, np.full(n, 64), (r[6] & np.uint64(0xFFFF)).astype(np.int64), ttl, 6,
@@ -279,15 +310,31 @@ def make_vxlan(n: int, seed: int = 0x5EED0004) -> PacketBatch:
     a[:, 96] = 0x50
     a[:, 97] = 0x18
     _be16(a, 98, np.full(n, 0x2000))
-    a[:, 104:128] = _rand_bytes(seed, 102, n, 24)
+    a[:, 104:128] = _rand_bytes(seed, 102, n, 24, base)
     _l4_checksum(a, 64, 84, 44, 6, 16)
     # outer UDP checksum 0 ("not computed"), as VXLAN encapsulators commonly send
-    bad = np.nonzero((np.arange(n) % 64) == 63)[0]
+    bad = np.nonzero(((np.arange(n) + base) % 64) == 63)[0]
     _corrupt(a, bad, 84 + 16)
-    data = np.zeros(n * 128 + PAD, dtype=np.uint8)
-    data[: n * 128] = a.reshape(-1)
-    return PacketBatch(data, n * 128, (np.arange(n, dtype=np.uint64) * 128).astype(np.uint32),
-                       np.full(n, 128, dtype=np.uint32))
+
+
+def make_vxlan(n: int, seed: int = 0x5EED0004, chunk: int = 1 << 17) -> PacketBatch:
+    """Config 4: 128 B Eth/IPv4/UDP(4789)/VXLAN/Eth/IPv4/TCP (104 B of headers + 24 B payload)."""
+    free_u, free_t = _free_ports(TABLES.udp_port), _free_ports(TABLES.tcp_port)
+    return _fixed_rows(n, 128, lambda a, base: _vxlan_rows(a, seed, base, free_u, free_t), chunk)
+
+
+def make_tcp64(n: int, seed: int = 0x5EED0008, chunk: int = 1 << 18) -> PacketBatch:
+    """The north star's literal target: 64 B Eth/IPv4/TCP frames (IHL 5, a 20-B TCP header with
+    ACK(+PSH), 10 payload bytes), seed 0x5EED0008; valid checksums except the TCP checksum of 1
+    packet in 64.  Not one of BASELINE.json's configs: config 2 is the same size over UDP."""
+    free = _free_ports(TABLES.tcp_port)
+
+    def fill(a, base):
+        m = a.shape[0]
+        r = [splitmix64(seed, m, j, base) for j in range(6)]
+        bad = np.nonzero(((np.arange(m) + base) % 64) == 63)[0]
+        a[:] = _tcp_frames(m, 64, r, np.zeros(0, np.int64), False, free, bad, seed, 400, base)
+    return _fixed_rows(n, 64, fill, chunk)
 
 
 # ---- a traffic mix with the rarer stacks and the generic decoder's share -------------------

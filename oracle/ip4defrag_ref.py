@@ -1,4 +1,7 @@
-"""ip4defrag's IPv4Defragmenter over the GPU fragment hand-off (host side).
+"""TEST INFRASTRUCTURE ONLY: ip4defrag's IPv4Defragmenter restated over the GPU fragment
+hand-off's records.  Only tests/ use it, as the checker that the hand-off (gpd_ip4_fragments,
+the product) gives a defragmenter everything it needs: ip4defrag's stateful reassembly is OUT
+OF SCOPE for the engine, so this lives beside the oracles, not in the package.
 
 The reference reassembles IPv4 datagrams in ip4defrag/defrag.go: `DefragIPv4WithTimestamp`
 (:86-135) filters with dontDefrag (:162-172), rejects with securityChecks (:175-198), files
@@ -23,7 +26,7 @@ from __future__ import annotations
 from dataclasses import dataclass, field
 from typing import List, Optional, Tuple
 
-from .defrag import FRAG_INSERT, FRAG_WHOLE, frag_error
+from gopacket_amd.defrag import FRAG_INSERT, FRAG_WHOLE, frag_error
 
 IPv4MinimumFragmentSize = 8
 IPv4MaximumSize = 65535

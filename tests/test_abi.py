@@ -122,3 +122,13 @@ def test_c_host_program_on_the_abi(tmp_path):
         assert words[:3] == ["abi_host", "ok", str(b.n)], r.stdout
         assert int(words[3]) > 100, r.stdout  # the mixed traffic holds many TCP/UDP flows
         assert int(words[4]) > 100, r.stdout  # ip4defrag's fragments and the fuzz frames
+
+
+def test_integration_build_command_names_every_source():
+    """INTEGRATION.md §1's single hipcc command must name every file build.py compiles."""
+    import re
+    from gopacket_amd.build import SOURCES
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    cmd = re.search(r"```sh\nhipcc .*?```", text, re.S).group(0)
+    for src in SOURCES:
+        assert os.path.relpath(src, ROOT) in cmd, src

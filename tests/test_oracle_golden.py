@@ -106,7 +106,7 @@ def test_pcap_test_dns():
 
 
 @pytest.mark.parametrize("maker,n", [(synth.make_udp64, 4096), (synth.make_imix, 4096),
-                                     (synth.make_vxlan, 4096)])
+                                     (synth.make_vxlan, 4096), (synth.make_tcp64, 4096)])
 def test_synthetic_configs_under_oracle(maker, n):
     b = maker(n)
     res = O.decode(b, L.LayerTypeEthernet, 0x3FF, ext=False)
@@ -125,3 +125,8 @@ def test_synthetic_configs_under_oracle(maker, n):
         if maker is synth.make_vxlan:
             for i in range(0, n, 97):
                 assert res.decoded(i) == [17, 20, 45, 116, 17, 20, 44, 2]
+        if maker is synth.make_tcp64:
+            for i in range(0, n, 97):
+                assert res.decoded(i) == [17, 20, 44, 2]
+            stored = np.array([struct.unpack(">H", b.packet(i)[24:26])[0] for i in range(n)])
+            assert np.array_equal(res.csum & 0xFFFF, stored)

@@ -150,7 +150,8 @@ def test_fuzz_random_headers():
     run_both(PacketBatch.from_packets(pkts), L.LayerTypeEthernet, ALL, 0)
 
 
-@pytest.mark.parametrize("maker", [synth.make_udp64, synth.make_imix, synth.make_vxlan, synth.make_mixed])
+@pytest.mark.parametrize("maker", [synth.make_udp64, synth.make_imix, synth.make_vxlan, synth.make_mixed,
+                                   synth.make_tcp64])
 def test_synthetic_configs(maker):
     b = maker(1 << 15)
     run_both(b, ext=True)
@@ -295,35 +296,66 @@ def test_decode_layers_single_packet_api():
     assert err is None and p2.Truncated and decoded == [17, 15, 20, 45, 2]
 
 
-def test_full_size_config2_properties():
-    """BASELINE config 2 at full size (2^24 packets): size-independent properties, plus a
-    bit-exact oracle comparison on a strided sample."""
+def _oracle_threads() -> int:
+    """The cores this process may use (affinity, capped by a cgroup v2 quota)."""
+    import os
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, -(-int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return max(1, min(n, 64))
+
+
+def _full_size_exact(b):
+    """Every packet of a full-size batch, all five result words and hdr_off, in the gpd_record
+    (AoS) form the bench times and in the SoA form, against the multi-threaded oracle.  Returns
+    the SoA result for the property checks."""
     import torch
     from gopacket_amd import parser as P
+    ref = O.decode(b, L.LayerTypeEthernet, ALL, 0, ext=False, nthreads=_oracle_threads())
+    p = _parser()
+    db = P.DeviceBatch(b, 0)
+    res = None
+    for records in (True, False):
+        dr = P.DeviceResult(b.n, 0, hdr_off=True, records=records)
+        p.decode_device(db, dr)
+        torch.cuda.synchronize()
+        res = dr.to_host()
+        del dr
+        assert_same(res, ref, b, ext=False)
+    del db, ref
+    torch.cuda.empty_cache()
+    return res
+
+
+def test_full_size_config2_exact():
+    """BASELINE config 2 at full size (2^24 x 64 B Eth/IPv4/UDP): every packet bit-exact against
+    the oracle in both result forms, plus the size-independent properties."""
     n = 1 << 24
     b = synth.make_udp64(n)
-    p = P.DecodingLayerParser(L.LayerTypeEthernet)
-    p._mask = ALL
-    res = p.DecodeBatch(b, ext=False)
+    res = _full_size_exact(b)
     assert np.all(res.status & 3 == 0)
     assert np.all(((res.status >> 4) & 31) == 4)
     bad = (np.arange(n) % 64) == 63
     stored = (b.data[24:n * 64:64].astype(np.uint32) << 8) | b.data[25:n * 64:64]
     assert np.array_equal((res.csum & 0xFFFF) == stored, ~bad)
     assert np.all(res.csum >> 16 == 0)
-    # sample
-    idx = np.arange(0, n, 4099)
-    sb = PacketBatch(b.data, b.data_len, b.offset[idx].copy(), b.caplen[idx].copy())
-    ref = O.decode(sb, ext=False, nthreads=8)
-    for f in ("status", "layers", "net_hash", "tp_hash", "csum"):
-        assert np.array_equal(getattr(res, f)[idx], getattr(ref, f)), f
-    del res
-    torch.cuda.empty_cache()
+
+
+def test_full_size_tcp64_exact():
+    """The north star's literal target at the bench's size (2^24 x 64 B Eth/IPv4/TCP): every
+    packet bit-exact in both result forms; TCP ComputeChecksum 0 exactly on the valid ones."""
+    n = 1 << 24
+    b = synth.make_tcp64(n)
+    res = _full_size_exact(b)
+    _full_size_common(b, res, [17, 20, 44, 2], 14, n)
 
 
 def _full_size_common(b, res, want_decoded, ip_off, n):
-    """Properties every packet of a full-size synthetic config shares, plus a strided sample
-    bit-exact against the oracle."""
+    """Properties every packet of a full-size synthetic config shares."""
     assert np.all(res.status & 3 == 0), "every packet decodes cleanly"
     assert np.all(((res.status >> 4) & 31) == len(want_decoded))
     assert np.all(res.layers == res.layers[0]), "one decoded stack for all"
@@ -333,46 +365,31 @@ def _full_size_common(b, res, want_decoded, ip_off, n):
     off = b.offset.astype(np.int64) + ip_off + 10
     stored = (b.data[off].astype(np.uint32) << 8) | b.data[off + 1]
     assert np.array_equal(res.csum & 0xFFFF, stored), "IPv4 header checksum equals the stored one"
-    idx = np.arange(0, n, 2039)
-    sb = PacketBatch(b.data, b.data_len, b.offset[idx].copy(), b.caplen[idx].copy())
-    ref = O.decode(sb, ext=False, nthreads=8)
-    for f in ("status", "layers", "net_hash", "tp_hash", "csum"):
-        assert np.array_equal(getattr(res, f)[idx], getattr(ref, f)), f
 
 
-def test_full_size_config3_imix_properties():
+def test_full_size_config3_imix_exact():
     """BASELINE config 3 at full size (2^22 IMIX 64/576/1500 Eth/Dot1Q/IPv4/TCP): every window
-    class, multi-window tiles and the wave-cooperative transport checksum at their real mix."""
-    import torch
-    from gopacket_amd import parser as P
+    class, multi-window tiles and the wave-cooperative transport checksum at their real mix;
+    every packet bit-exact in both result forms."""
     n = 1 << 22
     b = synth.make_imix(n)
-    p = P.DecodingLayerParser(L.LayerTypeEthernet)
-    p._mask = ALL
-    res = p.DecodeBatch(b, ext=False)
+    res = _full_size_exact(b)
     _full_size_common(b, res, [17, 15, 20, 44, 2], 18, n)
     # (the transport FastHash is symmetric in the two ports, so port pairs share values)
     assert len(np.unique(res.net_hash)) > n // 2 and len(np.unique(res.tp_hash)) > n // 64
-    del res
-    torch.cuda.empty_cache()
 
 
-def test_full_size_config4_vxlan_properties():
+def test_full_size_config4_vxlan_exact():
     """BASELINE config 4 at full size (2^23 x 128 B VXLAN): the two-pass stack
-    [Eth, IPv4, UDP, VXLAN, Eth, IPv4, TCP, Payload] on every packet, inner flow keys (A11)."""
-    import torch
-    from gopacket_amd import parser as P
+    [Eth, IPv4, UDP, VXLAN, Eth, IPv4, TCP, Payload] on every packet, inner flow keys (A11);
+    every packet bit-exact in both result forms."""
     n = 1 << 23
     b = synth.make_vxlan(n)
-    p = P.DecodingLayerParser(L.LayerTypeEthernet)
-    p._mask = ALL
-    res = p.DecodeBatch(b, ext=False)
+    res = _full_size_exact(b)
     _full_size_common(b, res, [17, 20, 45, 116, 17, 20, 44, 2], 64, n)
     # the flow keys are the inner 5-tuple: the inner addresses and ports of packet 0
     ref0 = O.decode(PacketBatch.from_packets([b.packet(0)[50:]]), ext=False)
     assert int(res.net_hash[0]) == int(ref0.net_hash[0]) and int(res.tp_hash[0]) == int(ref0.tp_hash[0])
-    del res
-    torch.cuda.empty_cache()
 
 
 @pytest.mark.parametrize("mask", [ALL, 0x3FF])
