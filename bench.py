@@ -93,6 +93,18 @@ def host_cores():
     return aff, os.cpu_count() or 1, quota
 
 
+def rank_threads(args) -> int:
+    """Host threads for this rank's host work (capture generation, record walks): --threads,
+    else the cores this process may use (affinity, capped by a cgroup quota) shared by the
+    node's ranks (LOCAL_WORLD_SIZE), at least 1."""
+    if args.threads:
+        return args.threads
+    aff, _, quota = host_cores()
+    cores = min(aff, max(1, int(-(-quota // 1)))) if quota else aff
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
+    return max(1, min(64, cores) // max(1, local_world))
+
+
 def _time_oracle(batch, decoders, threads, budget_s, out):
     import oracle_ref as O
     O.decode(batch, decoders=decoders, ext=False, nthreads=threads, out=out)  # warm
@@ -272,7 +284,7 @@ def bench_side(config, parser, args, local, stream):
     interleaved = 0
     if config == "pcap64":  # the capture bytes are the batch buffer (16-B record headers between)
         from gopacket_amd import pcap as NP
-        pc = NP.index(batch, nthreads=args.threads)
+        pc = NP.index(batch, nthreads=rank_threads(args))
         assert pc.err is None and pc.batch.n == n, (pc.err, pc.batch.n)
         batch, interleaved = pc.batch, 16
     t_gen = time.perf_counter() - t0
@@ -536,21 +548,39 @@ REPLAY_CHUNK = 1 << 24   # records per device index chunk and per gpd_decode_pca
 REPLAY_SEED = 0x5EED0002
 
 
-def host_buffer(nbytes: int, world: int, local: int, key: str, dist):
-    """The capture's host memory: private (one rank) or one shared mapping for all the node's
+def shm_fits(nbytes: int) -> bool:
+    st = os.statvfs("/dev/shm")
+    return st.f_bavail * st.f_frsize >= nbytes
+
+
+def capture_memory(args, nbytes: int, world: int, rank: int, dist, bcast_device) -> str:
+    """Where the capture lives: "private" (one rank, or --capture-memory private, or /dev/shm
+    too small for the whole capture on this node) or "shared" (one /dev/shm mapping for the
+    node's ranks).  Rank 0 decides for all (one broadcast), so the ranks agree."""
+    if world == 1:
+        return "private"
+    mode = args.capture_memory
+    if mode == "auto":
+        mode = "shared" if shm_fits(nbytes) else "private"
+    if dist:
+        import torch
+        t = torch.tensor([1 if mode == "shared" else 0], dtype=torch.int64, device=bcast_device)
+        dist.broadcast(t, 0)
+        mode = "shared" if int(t.item()) else "private"
+    return mode
+
+
+def host_buffer(nbytes: int, shared: bool, local: int, key: str, dist):
+    """The capture's host memory: private (anonymous) or one shared mapping for all the node's
     ranks (a /dev/shm file created by local rank 0).  Huge pages are asked for; returns
     (uint8 array, mmap object, path or None)."""
     import mmap
     path = None
-    if world == 1:
+    if not shared:
         mm = mmap.mmap(-1, nbytes)
     else:
         path = os.path.join("/dev/shm", f"gpd_replay_{key}")
         if local == 0:
-            st = os.statvfs("/dev/shm")
-            if st.f_bavail * st.f_frsize < nbytes:
-                raise SystemExit(f"bench: /dev/shm has {st.f_bavail * st.f_frsize} bytes free, the "
-                                 f"shared capture needs {nbytes}")
             with open(path, "wb") as f:
                 f.truncate(nbytes)
         dist.barrier()
@@ -564,30 +594,73 @@ def host_buffer(nbytes: int, world: int, local: int, key: str, dist):
     return np.frombuffer(mm, np.uint8), mm, path
 
 
-def build_replay_capture(n: int, world: int, rank: int, local: int, key: str, dist, threads: int):
-    """ONE seeded capture (pcapgo framing, LE microseconds, snaplen 262144): records i = 0..n-1
-    are config 2's packets (synth.make_udp64(seed 0x5EED0002) packet i), each behind its 16-B
-    record header.  The ranks write disjoint record ranges of the one buffer in parallel (setup,
-    untimed); the decode side finds the shards by walking the records (gpd_pcap_locate)."""
-    import struct
-    from gopacket_amd import synth
-    from gopacket_amd.batch import PAD
-    nbytes = 24 + 80 * n + PAD
-    cap, mm, path = host_buffer(nbytes, world, local, key, dist)
-    try:
-        lo, hi = n * rank // world, n * (rank + 1) // world
-        if rank == 0:
-            cap[:24] = np.frombuffer(struct.pack("<IHHiIII", 0xA1B2C3D4, 2, 4, 0, 0, 262144, 1),
-                                     np.uint8)
-        synth.udp64_native(cap[24 + 80 * lo:24 + 80 * hi], lo, hi, REPLAY_SEED, records=True,
-                           nthreads=threads)
-        cap[24 + 80 * n:] = 0
-        if dist:
+PCAP_FILE_HEADER = (0xA1B2C3D4, 2, 4, 0, 0, 262144, 1)  # pcapgo framing: LE, microseconds
+
+
+class ReplayCapture:
+    """This rank's view of config 5's ONE seeded capture (pcapgo framing, LE microseconds,
+    snaplen 262144): records i = 0..n-1 are config 2's packets (synth.make_udp64(seed
+    0x5EED0002) packet i), each behind its 16-B record header.
+
+    shared: the whole capture in one /dev/shm mapping; the ranks write disjoint record ranges
+      in parallel (setup, untimed), and rank 0 finds the shard cuts by walking the records
+      (gpd_pcap_locate) and broadcasts them.
+    private (/dev/shm too small for the node, e.g. 80 GB for 10^9 records): each rank builds
+      only its own shard [g*N/G, (g+1)*N/G) — the file header followed by exactly those records,
+      byte-identical to that stretch of the whole capture — in private memory.  The cut is
+      then where the shard's bytes start (the records are fixed 80-B synthetic records, so
+      record g*N/G of the whole capture sits at 24 + 80*(g*N/G)); the rank still walks its
+      own records for the chunk boundaries, and `base` maps its positions to the whole
+      capture's.
+    `cap` is the rank's buffer, [start, end) its shard's records in it."""
+
+    def __init__(self, args, n: int, world: int, rank: int, local: int, dist, threads: int,
+                 bcast_device):
+        import struct
+        from gopacket_amd import pcap as NP
+        from gopacket_amd import synth
+        from gopacket_amd.batch import PAD
+        self.n = n
+        key = f"{REPLAY_SEED:x}_{n}_{os.environ.get('MASTER_PORT', '0')}"
+        lo, hi = NP.shard_bounds(n, world)[rank]
+        self.mode = capture_memory(args, 24 + 80 * n + PAD, world, rank, dist, bcast_device)
+        hdr = np.frombuffer(struct.pack("<IHHiIII", *PCAP_FILE_HEADER), np.uint8)
+        if self.mode == "private":
+            m = hi - lo
+            cap, mm, _ = host_buffer(24 + 80 * m + PAD, False, local, key, dist)
+            cap[:24] = hdr
+            synth.udp64_native(cap[24:24 + 80 * m], lo, hi, REPLAY_SEED, records=True, nthreads=threads)
+            cap[24 + 80 * m:] = 0
+            self.cap, self.mm = cap, mm
+            self.start, self.end, self.base = 24, 24 + 80 * m, 80 * lo
+            self.data_len = 24 + 80 * m
+            if dist:
+                dist.barrier()
+            return
+        cap, mm, path = host_buffer(24 + 80 * n + PAD, True, local, key, dist)
+        try:
+            if rank == 0:
+                cap[:24] = hdr
+            synth.udp64_native(cap[24 + 80 * lo:24 + 80 * hi], lo, hi, REPLAY_SEED, records=True,
+                               nthreads=threads)
+            cap[24 + 80 * n:] = 0
             dist.barrier()
-    finally:  # every rank has mapped the file: its name is no longer needed
-        if path and local == 0 and os.path.exists(path):
-            os.unlink(path)
-    return cap, mm
+        finally:  # every rank has mapped the file: its name is no longer needed
+            if path and local == 0 and os.path.exists(path):
+                os.unlink(path)
+        self.cap, self.mm, self.base, self.data_len = cap, mm, 0, 24 + 80 * n
+        bounds = NP.shard_bounds(n, world)
+        if rank == 0:
+            pos, total, stop = NP.locate(cap, [b for b, _ in bounds] + [n], data_len=self.data_len,
+                                         nthreads=threads)
+            assert total == n and stop == NP.STOP_EOF, (total, stop)
+        else:
+            pos = np.zeros(world + 1, np.uint64)
+        import torch
+        pt = torch.from_numpy(pos.view(np.int64).copy()).to(bcast_device)
+        dist.broadcast(pt, 0)
+        pos = pt.cpu().numpy().view(np.uint64)
+        self.start, self.end = int(pos[rank]), int(pos[rank + 1])
 
 
 class _Res:
@@ -655,28 +728,18 @@ def bench_replay(args, world, rank, local, dist):
     from gopacket_amd._lib import GpdBatch, check, lib
     from gopacket_amd.results import BatchResult
     n = args.packets or 10 ** 9
-    threads = args.threads or 16
-    key = f"{REPLAY_SEED:x}_{n}_{os.environ.get('MASTER_PORT', '0')}"
+    threads = rank_threads(args)
+    dev = torch.device("cuda", local)
     t0 = time.perf_counter()
     host_local = int(os.environ.get("LOCAL_RANK", local))  # the host roles (--same-device keeps them)
-    cap, mm = build_replay_capture(n, world, rank, host_local, key, dist, threads)
+    rc = ReplayCapture(args, n, world, rank, host_local, dist, threads, COMM_DEVICE or dev)
+    cap, mm = rc.cap, rc.mm
     t_gen = time.perf_counter() - t0
-    dl = 24 + 80 * n
+    dl = rc.data_len
     info = NP.header(cap, dl)
-    dev = torch.device("cuda", local)
-    # the cut: shard g = records [g*N/G, (g+1)*N/G), found by walking the records
     t0 = time.perf_counter()
+    start, end = rc.start, rc.end
     bounds = NP.shard_bounds(n, world)
-    if rank == 0:
-        pos, total, stop = NP.locate(cap, [lo for lo, _ in bounds] + [n], data_len=dl, nthreads=threads)
-        assert total == n and stop == NP.STOP_EOF, (total, stop)
-    else:
-        pos = np.zeros(world + 1, np.uint64)
-    if dist:
-        pt = torch.from_numpy(pos.view(np.int64).copy()).to(COMM_DEVICE or dev)
-        dist.broadcast(pt, 0)
-        pos = pt.cpu().numpy().view(np.uint64)
-    start, end = int(pos[rank]), int(pos[rank + 1])
     lo, hi = bounds[rank]
     m = hi - lo
     chunks = [(c, min(c + REPLAY_CHUNK, m)) for c in range(0, m, REPLAY_CHUNK)]
@@ -826,7 +889,10 @@ def bench_replay(args, world, rank, local, dist):
                                f"by packet index over {world} GPU(s) (gpd_pcap_locate), each shard "
                                f"resident in HBM and decoded in place in 2^24-record launches",
                    "packets_total": n, "parallelism": f"shard{world}", "chunk_records": REPLAY_CHUNK,
-                   "capture_bytes": dl, "capture_memory": "private" if world == 1 else "/dev/shm (shared)",
+                   "capture_bytes": 24 + 80 * n,
+                   "capture_memory": {"private": "private (each rank builds its own shard's records)",
+                                      "shared": "/dev/shm (shared)"}[rc.mode],
+                   "host_threads_per_rank": threads,
                    "read_bytes_per_packet": round(rb0 / m0, 2), "result_bytes_per_packet": write_per,
                    "result_form": "gpd_record (AoS)" if aos else "SoA arrays", "settle_ms": settled,
                    "decode_errors": int(sum(r[5] for r in rows))},
@@ -857,25 +923,14 @@ def shard_check(args, world, rank, local, dist):
     bench_replay builds it, shard g located and indexed chunk by chunk, its records' header
     positions written to <dir>/rank<g>.npz."""
     from gopacket_amd import pcap as NP
-    import torch
     n = args.packets or 10 ** 9
-    threads = args.threads or 4
-    key = f"{REPLAY_SEED:x}_{n}_{os.environ.get('MASTER_PORT', '0')}"
+    threads = rank_threads(args)
     host_local = int(os.environ.get("LOCAL_RANK", local))  # the host roles (--same-device keeps them)
-    cap, mm = build_replay_capture(n, world, rank, host_local, key, dist, threads)
-    dl = 24 + 80 * n
-    info = NP.header(cap, dl)
+    rc = ReplayCapture(args, n, world, rank, host_local, dist, threads, "cpu")
+    cap, mm = rc.cap, rc.mm
+    info = NP.header(cap, rc.data_len)
     bounds = NP.shard_bounds(n, world)
-    if rank == 0:
-        pos, total, stop = NP.locate(cap, [lo for lo, _ in bounds] + [n], data_len=dl, nthreads=threads)
-        assert total == n and stop == NP.STOP_EOF
-    else:
-        pos = np.zeros(world + 1, np.uint64)
-    if dist:
-        pt = torch.from_numpy(pos.view(np.int64).copy())
-        dist.broadcast(pt, 0)
-        pos = pt.numpy().view(np.uint64)
-    start, end = int(pos[rank]), int(pos[rank + 1])
+    start, end = rc.start, rc.end
     lo, hi = bounds[rank]
     m = hi - lo
     chunk = args.chunk or REPLAY_CHUNK
@@ -888,9 +943,10 @@ def shard_check(args, world, rank, local, dist):
         pc = NP.index(cap[base:], max_n=b - a, nthreads=threads, data_len=int(cpos[k + 1]) - base,
                       pos=hdr - base, info=info)
         assert pc.batch.n == b - a and pc.err is None
-        hdrs.append(pc.batch.offset.astype(np.uint64) + base - 16)
+        hdrs.append(pc.batch.offset.astype(np.uint64) + base - 16 + rc.base)  # whole-capture positions
     np.savez(os.path.join(args.shard_check, f"rank{rank}.npz"), hdr=np.concatenate(hdrs) if hdrs else
-             np.zeros(0, np.uint64), lo=lo, hi=hi, start=start, end=end, world=world, cn=cn)
+             np.zeros(0, np.uint64), lo=lo, hi=hi, start=start + rc.base, end=end + rc.base, world=world,
+             cn=cn, mode=rc.mode, threads=threads)
     if dist:
         dist.barrier()
 
@@ -953,6 +1009,10 @@ def main():
     ap.add_argument("--shard-check", default="", help="tests only (CPU, gloo): build the replay "
                     "capture, cut and index this rank's shard, write its record positions to DIR")
     ap.add_argument("--chunk", type=int, default=0, help="tests only: records per index chunk")
+    ap.add_argument("--capture-memory", default="auto", choices=("auto", "shared", "private"),
+                    help="replay with N > 1: the whole capture in one /dev/shm mapping (shared) or "
+                         "each rank's shard in private memory (private); auto = shared when "
+                         "/dev/shm has room for the whole capture")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="tests only: gloo rehearses the N-rank path without RCCL")
     ap.add_argument("--same-device", action="store_true",
@@ -1013,7 +1073,7 @@ def main():
         from gopacket_amd import pcap as NP
         cap = batch
         t0 = time.perf_counter()
-        pc = NP.index(cap, nthreads=args.threads)
+        pc = NP.index(cap, nthreads=rank_threads(args))
         t_index = time.perf_counter() - t0
         assert pc.err is None and pc.batch.n == n, (pc.err, pc.batch.n)
         batch = pc.batch
@@ -1119,7 +1179,7 @@ def main():
     if pcap_info:
         out["pcap"] = pcap_info
         if args.replay:
-            out["pcap"]["pcie_inclusive"] = replay_pcap(parser, cap, n, args.replay, args.threads)
+            out["pcap"]["pcie_inclusive"] = replay_pcap(parser, cap, n, args.replay, rank_threads(args))
     tr = load_traffic(args.config) if n == n_default else None
     if tr and tr["read"] and tr["write"]:  # PMC bytes, same read+write scope as `achieved`
         out["roofline"]["traffic"] = int(tr["read"]) + int(tr["write"])

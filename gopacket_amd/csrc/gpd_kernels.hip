@@ -50,6 +50,12 @@ constexpr uint32_t kRegPrefix = 1u << 26;       // internal: 8 KiB windows of lo
 constexpr uint32_t kHeaderOnce = 1u << 25;      // internal: 8 KiB windows decoded once per tile (seg_pass)
 constexpr uint32_t kDiagMask = kDiagSkipDecode | kDiagNoWait | kDiagNtLoad | kDiagNtStore | kShiftWindows |
                                kRegPrefix | kHeaderOnce;
+// A/B builds only (GPD_EXTRA_CFLAGS=-DGPD_EXP=..., tools/ab_exp.sh): fast-path variants
+#ifndef GPD_EXP
+#define GPD_EXP 0
+#endif
+constexpr uint32_t kExp = GPD_EXP;
+constexpr uint32_t kExpE = 8u;  // AL: the outer pass's header bytes from five aligned chunks
 
 extern __shared__ __attribute__((aligned(16))) uint8_t g_lds[];
 
@@ -1015,7 +1021,7 @@ __device__ __forceinline__ void seg_pass(uint32_t p, uint32_t len, uint32_t buf,
 // COOP: a long even-aligned segment's whole middle chunks are left to window_prefix (sg).
 // HO: the header-once decode — no window is read: the header bytes and the segment sum come
 // from seg_pass (*h), one pass (a VXLAN payload takes the generic decoder).
-template <bool CS, bool HASH, bool COOP, bool HO = false>
+template <bool CS, bool HASH, bool COOP, bool HO = false, bool AL = false>
 __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const FastCtx &F, Out &o,
                                             uint32_t buf, Seg &sg, const Hdr *h = nullptr) {
   uint64_t codes = 0, nh = 0, th = 0;
@@ -1025,6 +1031,12 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
   uint32_t tp_kind = 0, ps4 = 0, ps6 = 0;      // its network object kind; each kind's addresses
   uint32_t net_off = 0;                        // the last network header
   uint32_t b = 0, lim = len;                   // this pass's Ethernet offset; end of its data
+  // AL (unshifted 8 KiB windows, frames of ~65..160 B): a VXLAN frame's inner Ethernet bytes
+  // 8..23 come from the outer pass's registers when it is IPv4 (IHL 5) / UDP / VXLAN — one
+  // misaligned LDS read fewer per pass (VXLAN -1.8 %; in the other kernels the longer live
+  // range costs 1-5 %, measured A/B on one box)
+  constexpr bool reg_e = !HO && AL;
+  uint32_t ie1 = 0, ie2 = 0, ie3 = 0, have_ie = 0;
   auto put = [&](uint32_t code) { codes |= (uint64_t)code << (16 + 4 * nc); nc++; };
   for (int pass = 0; pass < (HO ? 1 : 2); pass++) {
     // ---- round trip 1: Ethernet header (ethernet.go:41-62) and the bytes after it
@@ -1038,6 +1050,24 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
       e.w = h->e3;
 #pragma unroll
       for (int k = 0; k < 16; k++) W[k] = h->W[k];
+    } else if (reg_e && have_ie) {
+      e.x = 0;
+      e.y = ie1;
+      e.z = ie2;
+      e.w = ie3;
+      load64(W, p + b + 14);
+    } else if ((kExp & kExpE) && AL && pass == 0 && __all((p & 15u) == 0u)) {
+      // the frame's bytes 0..79 as five aligned 16-byte reads (~1/3.6 the cost of the five
+      // misaligned ones at bytes 8 and 14), the header words assembled with v_alignbyte
+      uint32_t x[20];
+#pragma unroll
+      for (int k = 0; k < 5; k++) {
+        const uint4 q = *reinterpret_cast<const uint4 *>(g_lds + p + 16u * k);
+        x[4 * k] = q.x; x[4 * k + 1] = q.y; x[4 * k + 2] = q.z; x[4 * k + 3] = q.w;
+      }
+      e.x = x[2]; e.y = x[3]; e.z = x[4]; e.w = x[5];
+#pragma unroll
+      for (int k = 0; k < 16; k++) W[k] = __builtin_amdgcn_alignbyte(x[4 + k], x[3 + k], 2u);
     } else {
       e = ld128(p + b + 8);
       load64(W, p + b + 14);
@@ -1184,7 +1214,14 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
     put(GPD_C_VXLAN);  // vxlan.go:53-78; its payload is an Ethernet frame (A11: two passes)
     b = l4 + hl + 8;
     if (pl4 == 8u) break;
+    if (reg_e) {  // IPv4 (IHL 5) / UDP / VXLAN: the inner bytes 8..23 are W[11..14]
+      have_ie = (v4 && g == 2u) ? 1u : 0u;
+      ie1 = W[12];
+      ie2 = W[13];
+      ie3 = W[14];
+    }
   }
+
   // ---- outputs, composed exactly as decode_packet does
   const uint32_t tp_ps = tp_pl + (tp_kind == 1u ? ps4 : ps6);
   uint32_t st = (stop ? F.unsup : GPD_ST_OK) | (trunc << 2) | (nc << 4);
@@ -1232,6 +1269,50 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
     o.csum = ip4 ? ipcs : 0u;  // the transport half is added by the caller
     o.hoff = hdr_word(net != 0, net_off, tp != 0, tp_off);
     return true;
+  } else if (AL && CS && tp && !((p + tp_off) & 1u)) {
+    // AL (unshifted 8 KiB windows, VXLAN-sized frames): the same sum from aligned 16-byte
+    // chunks, head [S, A) and tail [B, E) masked and the whole chunks between as they are — an
+    // aligned DS read costs ~1/3.6 of a misaligned one (VXLAN -3.4 %; with shifted copies of
+    // small frames the header reads are aligned already and the masking cost pcap64 +1 %,
+    // measured A/B on one box)
+    const uint32_t S = p + tp_off, E = S + tp_len, A = (S + 15u) & ~15u, B = E & ~15u;
+    uint32_t s = tp_ps;
+    if (A > S) {
+      const uint4 q = *reinterpret_cast<const uint4 *>(g_lds + A - 16u);
+      const uint32_t h8 = (S & 15u) * 8u;
+      const uint32_t e8 = E < A ? (A - E) * 8u : 0u;  // a segment ending inside its head chunk
+      uint64_t lo = ((uint64_t)q.y << 32) | q.x, hi = ((uint64_t)q.w << 32) | q.z;
+      lo = h8 >= 64u ? 0ull : (lo >> h8) << h8;
+      hi = h8 > 64u ? (hi >> (h8 - 64u)) << (h8 - 64u) : hi;
+      if (e8) {  // drop the e8 top bits of (hi, lo)
+        hi = e8 >= 64u ? 0ull : (hi << e8) >> e8;
+        lo = e8 > 64u ? (lo << (e8 - 64u)) >> (e8 - 64u) : lo;
+      }
+      s = dot2((uint32_t)lo, 0x00010001u, s);
+      s = dot2((uint32_t)(lo >> 32), 0x00010001u, s);
+      s = dot2((uint32_t)hi, 0x00010001u, s);
+      s = dot2((uint32_t)(hi >> 32), 0x00010001u, s);
+    }
+    for (uint32_t x = A; x < B; x += 16u) {
+      const uint4 q = *reinterpret_cast<const uint4 *>(g_lds + x);
+      s = dot2(q.x, 0x00010001u, s);
+      s = dot2(q.y, 0x00010001u, s);
+      s = dot2(q.z, 0x00010001u, s);
+      s = dot2(q.w, 0x00010001u, s);
+    }
+    if (E > B && B >= A) {
+      const uint4 q = *reinterpret_cast<const uint4 *>(g_lds + B);
+      const uint32_t r8 = (E & 15u) * 8u;
+      uint64_t lo = ((uint64_t)q.y << 32) | q.x, hi = ((uint64_t)q.w << 32) | q.z;
+      lo = r8 >= 64u ? lo : (lo << (64u - r8)) >> (64u - r8);
+      hi = r8 > 64u ? (hi << (128u - r8)) >> (128u - r8) : 0ull;
+      s = dot2((uint32_t)lo, 0x00010001u, s);
+      s = dot2((uint32_t)(lo >> 32), 0x00010001u, s);
+      s = dot2((uint32_t)hi, 0x00010001u, s);
+      s = dot2((uint32_t)(hi >> 32), 0x00010001u, s);
+    }
+    cs = (ip4 ? ipcs : 0u) | (fold_le_not(s) << 16);
+    st |= (ip4 ? 1u << 18 : 0u) | (1u << 19);
   } else if (CS) {
     // TCP.ComputeChecksum(), tcp.go:193-195 / tcpip.go:52-88 over the last transport.  Its
     // first and ragged-last 16-byte chunks are read here, once, after the parse (holding
@@ -1706,7 +1787,8 @@ __device__ __forceinline__ void rows_prefix(const uint32_t (&cs)[NC], uint32_t p
 // window finished (deferred one iteration, so that after the next window's loads nothing else
 // is issued and the wait at the next commit covers exactly those loads)  ->  plan and load
 // window k+1  ->  decode window k from LDS.
-template <int STAGE, bool CS, bool HASH, int MINW, bool DEFER = false, bool RPFX = true, bool HO = false>
+template <int STAGE, bool CS, bool HASH, int MINW, bool DEFER = false, bool RPFX = true, bool HO = false,
+          bool AL = false>
 __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
   constexpr int WAVES = 4;
   constexpr int NC = STAGE / 1024;              // 16-byte chunks per lane per window
@@ -1886,7 +1968,8 @@ __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
       if (HO) {
         seg_pass<COOP>(buf + wshift(Wd) + (off_d - Wd.base), end_d - off_d, buf, hh, sg, F, vxreg);
         got = 1;
-      } else if (!fast_decode<CS, HASH, COOP>(buf + wshift(Wd) + (off_d - Wd.base), end_d - off_d, F, res, buf, sg)) {
+      } else if (!fast_decode<CS, HASH, COOP, false, AL>(buf + wshift(Wd) + (off_d - Wd.base), end_d - off_d, F,
+                                                          res, buf, sg)) {
         fb = 1;
       }
     }
@@ -1900,7 +1983,8 @@ __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
         got = 2;
         if (__popcll(vxm) <= 16) {
           fb = 1;
-        } else if (!fast_decode<CS, HASH, COOP>(buf + wshift(Wd) + (off_d - Wd.base), end_d - off_d, F, res, buf, sg)) {
+        } else if (!fast_decode<CS, HASH, COOP, false, AL>(buf + wshift(Wd) + (off_d - Wd.base), end_d - off_d,
+                                                            F, res, buf, sg)) {
           fb = 1;
         }
       }
@@ -2017,7 +2101,8 @@ static hipError_t launch_t(const KParams &P, hipStream_t stream, int num_cus) {
   return hipGetLastError();
 }
 
-template <int STAGE, bool CS, bool HASH, int MINW, bool DEFER = false, bool RPFX = true, bool HO = false>
+template <int STAGE, bool CS, bool HASH, int MINW, bool DEFER = false, bool RPFX = true, bool HO = false,
+          bool AL = false>
 static hipError_t launch_rs(KParams &P, hipStream_t stream, int num_cus) {
   const uint64_t ntiles = (P.n + 63) / 64;
   const size_t lds = ((P.image_words * 4u + 15u) & ~15u) + 4 * (size_t)rs_wave_lds_bytes(STAGE) + 64;
@@ -2028,7 +2113,7 @@ static hipError_t launch_rs(KParams &P, hipStream_t stream, int num_cus) {
   P.fb_waves = (uint32_t)blocks * 4u;
   if (blocks == 0) return hipSuccess;
   if (P.fb_waves > (uint32_t)num_cus * kMaxFastWavesPerCU) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((rs_kernel<STAGE, CS, HASH, MINW, DEFER, RPFX, HO>), dim3((unsigned)blocks), dim3(256), lds, stream, P);
+  hipLaunchKernelGGL((rs_kernel<STAGE, CS, HASH, MINW, DEFER, RPFX, HO, AL>), dim3((unsigned)blocks), dim3(256), lds, stream, P);
   return hipGetLastError();
 }
 
@@ -2049,6 +2134,10 @@ static hipError_t launch_fast(KParams &P, hipStream_t stream, int num_cus) {
   }
   if (P.waves == 2) return launch_rs<8192, CS, HASH, 2>(P, stream, num_cus);
   if (P.options & kRegPrefix) return launch_rs<8192, CS, HASH, 3>(P, stream, num_cus);
+  // unshifted windows of mid-sized frames (VXLAN's 128 B): the aligned-chunk transport checksum
+  // and the inner Ethernet bytes from registers (fast_decode AL); shifted windows (pcap records,
+  // 65..96-B slots) keep the plain kernel, where both cost ~1 % (measured A/B)
+  if (!(P.options & kShiftWindows)) return launch_rs<8192, CS, HASH, 3, false, false, false, true>(P, stream, num_cus);
   return launch_rs<8192, CS, HASH, 3, false, false>(P, stream, num_cus);
 }
 

@@ -123,17 +123,29 @@ def _udp64_rows(a: np.ndarray, seed: int, base: int, free: np.ndarray) -> None:
     _corrupt(a, bad, 24)  # IPv4 header checksum byte
 
 
-def _parallel(jobs) -> None:
-    """Run independent chunk jobs on a thread pool: numpy's kernels release the GIL, and every
-    chunk's bytes depend only on (seed, stream, packet index), so the result is the same bytes
-    whatever the order."""
+def host_threads() -> int:
+    """Threads for host-side generation: the cores this process may use (affinity, capped by a
+    cgroup v2 quota, at most 16), shared by the node's ranks (LOCAL_WORLD_SIZE)."""
     import os
-    from concurrent.futures import ThreadPoolExecutor
     try:
         nt = len(os.sched_getaffinity(0))
     except AttributeError:
         nt = os.cpu_count() or 1
-    nt = max(1, min(16, nt, len(jobs)))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            nt = min(nt, max(1, -(-int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return max(1, min(16, nt) // max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1"))))
+
+
+def _parallel(jobs) -> None:
+    """Run independent chunk jobs on a thread pool: numpy's kernels release the GIL, and every
+    chunk's bytes depend only on (seed, stream, packet index), so the result is the same bytes
+    whatever the order."""
+    from concurrent.futures import ThreadPoolExecutor
+    nt = max(1, min(host_threads(), len(jobs)))
     if nt == 1:
         for j in jobs:
             j()

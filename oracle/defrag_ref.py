@@ -4,8 +4,10 @@ fragment hand-off oracle).
 Only tests/ may use this; the product path (gpd_ip4_fragments, include/gpd_defrag.h) never does.
 
 For every packet whose DecodeLayers left an IPv4 layer in `decoded`, the application calls
-IPv4Defragmenter.DefragIPv4(&ip4) (ip4defrag/defrag.go:76-135) with the parser's IPv4 object,
-whose state is that of its last successful DecodeFromBytes (the oracle's ext record, obj[2]).
+IPv4Defragmenter.DefragIPv4(&ip4) (ip4defrag/defrag.go:76-135) with the parser's IPv4 object as
+the call leaves it (the oracle's ext record, obj[2]): its last successful DecodeFromBytes, or a
+later IPv4 call that failed after assigning the header fields and Contents = data
+(ip4.go:195-210; e.g. IPv4-in-IPv4 with a broken inner header, tests/golden/errpath.json).
 DefragIPv4WithTimestamp:
   * returns the layer unchanged when dontDefrag holds (defrag.go:88-91,162-172):
     Flags & DontFragment, or neither MoreFragments nor a FragOffset;

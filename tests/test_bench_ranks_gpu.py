@@ -12,11 +12,11 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _bench(*args, timeout=300):
+def _bench(*args, gpus=2, timeout=300):
     env = dict(os.environ)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend",
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--dist-backend",
                         "gloo", "--same-device", "--no-cpu-baseline", "--settle-ms", "20", *args],
                        capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -26,21 +26,29 @@ def _bench(*args, timeout=300):
 
 
 @pytest.mark.gpu
-def test_two_ranks_weak_scaling_line():
-    d = _bench("--steps", "3", "--warmup", "1", "--packets", str(1 << 20))
-    assert d["n_gpus"] == 2 and d["scaling"] == "weak"
-    assert d["config"]["decode_errors_in_batch"] == 0 and d["config"]["packets_per_gpu"] == 1 << 20
-    # value = packets of both ranks over the max-over-ranks time
-    assert abs(d["value"] - 2 * (1 << 20) * 3 / (d["ms_per_step"] * 3 * 1e-3) / 1e6) / d["value"] < 0.02
+@pytest.mark.parametrize("gpus", [2, 8])
+def test_ranks_weak_scaling_line(gpus):
+    """The default line's N-rank path (8 = the driver's node, rehearsed on one GPU)."""
+    n = 1 << (20 if gpus == 2 else 18)
+    d = _bench("--steps", "3", "--warmup", "1", "--packets", str(n), gpus=gpus)
+    assert d["n_gpus"] == gpus and d["scaling"] == "weak"
+    assert d["config"]["decode_errors_in_batch"] == 0 and d["config"]["packets_per_gpu"] == n
+    # value = packets of all ranks over the max-over-ranks time
+    assert abs(d["value"] - gpus * n * 3 / (d["ms_per_step"] * 3 * 1e-3) / 1e6) / d["value"] < 0.02
 
 
 @pytest.mark.gpu
-def test_two_ranks_sharded_replay():
+@pytest.mark.parametrize("gpus,mem", [(2, "auto"), (8, "private"), (8, "shared")])
+def test_ranks_sharded_replay(gpus, mem):
+    """Config 5's cut and both legs with every rank; `private` is the fallback when /dev/shm
+    cannot hold the node's capture (each rank builds its own shard)."""
     n = 3 * (1 << 20) + 12345
-    d = _bench("--config", "replay", "--steps", "2", "--warmup", "1", "--packets", str(n))
-    assert d["n_gpus"] == 2 and d["scaling"] == "strong"
+    d = _bench("--config", "replay", "--steps", "2", "--warmup", "1", "--packets", str(n),
+               "--capture-memory", mem, gpus=gpus)
+    assert d["n_gpus"] == gpus and d["scaling"] == "strong"
     ranks = d["per_rank"]
-    assert [r["rank"] for r in ranks] == [0, 1]
+    assert [r["rank"] for r in ranks] == list(range(gpus))
     assert sum(r["packets"] for r in ranks) == n
     assert all(r["decode_errors"] == 0 and r["streamed_equals_resident"] for r in ranks)
-    assert len(d["roofline"]["read_frac_per_rank"]) == 2
+    assert len(d["roofline"]["read_frac_per_rank"]) == gpus
+    assert d["config"]["capture_memory"].startswith("private" if mem == "private" else "/dev/shm")

@@ -41,10 +41,16 @@ def _whole_capture(n):
     return cap
 
 
-@pytest.mark.parametrize("world,n,chunk", [(2, 200003, 30000), (3, 100000, 1 << 24)])
-def test_replay_shards_through_the_launcher(tmp_path, world, n, chunk):
+@pytest.mark.parametrize("world,n,chunk,mem,threads", [
+    (2, 200003, 30000, "auto", 2), (3, 100000, 1 << 24, "auto", 2),
+    (8, 400009, 20000, "shared", 0), (8, 400009, 20000, "private", 0), (3, 100000, 7000, "private", 2)])
+def test_replay_shards_through_the_launcher(tmp_path, world, n, chunk, mem, threads):
+    """World 8 is the driver's node: both capture memories (the private one is what a node whose
+    /dev/shm cannot hold the 80-GB capture falls back to), threads per rank by default (the
+    node's cores shared by its ranks)."""
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--config", "replay",
-           "--packets", str(n), "--chunk", str(chunk), "--threads", "2", "--shard-check", str(tmp_path)]
+           "--packets", str(n), "--chunk", str(chunk), "--threads", str(threads), "--capture-memory", mem,
+           "--shard-check", str(tmp_path)]
     env = dict(os.environ)
     env.pop("WORLD_SIZE", None)
     before = set(os.listdir("/dev/shm"))
@@ -56,6 +62,9 @@ def test_replay_shards_through_the_launcher(tmp_path, world, n, chunk):
     want = whole.batch.offset.astype(np.uint64) - 16
     # shard g holds records [g*N/G, (g+1)*N/G): disjoint, in order, together the whole index
     for g, p in enumerate(parts):
+        assert str(p["mode"]) == ("shared" if mem == "auto" else mem)
+        if threads == 0:
+            assert 1 <= int(p["threads"]) <= max(1, 16 // world) * 4
         assert (int(p["lo"]), int(p["hi"])) == (n * g // world, n * (g + 1) // world)
         assert int(p["world"]) == world and int(p["cn"]) == int(p["hi"]) - int(p["lo"])
         assert np.array_equal(p["hdr"], want[int(p["lo"]):int(p["hi"])])
