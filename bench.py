@@ -355,9 +355,10 @@ def bench_host(parser, batch, n, mode, steps, warmup):
 
 
 def bench_split(parser, dev_batch, dev_res, n, local, stream):
-    """The launch split in two (gpd_last_launch_split): how many packets the fast kernel left to
-    the generic list kernel (options, fragments, hop-by-hop, errors ...) and each kernel's
-    event-timed share of the launch (mean of 5)."""
+    """gpd_last_launch_split: how many packets the fast decode left to the generic decoder
+    (options, fragments, hop-by-hop, errors ...; each wave decodes its own list at its end, in
+    the same kernel) and the event-timed kernel time (mean of 5); list_kernel_ms is what the
+    launch spent after that kernel (~0 since the lists moved into it)."""
     import ctypes as C
 
     import torch

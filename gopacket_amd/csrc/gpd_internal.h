@@ -74,10 +74,9 @@ struct KParams {
   uint32_t nstores;            // store instructions per tile (non-NULL result arrays)
   uint32_t fixed;              // tables in the kFix* layout (eth_mult shared by all three)
   uint32_t waves;              // fast kernel waves per SIMD (0: the default for the window)
-  uint32_t *fb_count;          // fast kernel: 1 when any packet fell back (device scratch, zero)
-  uint32_t *fb_next;           // the flag the next fast launch uses (list_kernel zeroes it)
   uint32_t *fb_list;           // fast kernel: packet indices left to the generic decoder, in one
-                               // private region per wave (64 x its tiles; see rs_kernel)
+                               // private region per wave (64 x its tiles), which that wave
+                               // decodes after its tiles (see rs_kernel)
   uint32_t *fb_wcount;         // per fast-kernel wave: entries in its region
   uint32_t fb_waves;           // waves of the fast launch (set by launch_decode)
 };
@@ -85,8 +84,8 @@ struct KParams {
 // grid rounds x 4 waves): sizes fb_wcount.
 constexpr uint32_t kMaxFastWavesPerCU = 4 * 4 * 4;
 
-// True when launch_decode takes the fast kernel + fallback list (needs fb_count/fb_list
-// with room for P.n entries).
+// True when launch_decode takes the fast kernel (needs fb_list with room for P.n entries and
+// fb_wcount).
 bool fast_eligible(const KParams &P);
 
 // The pcap record walk on the GPU (gpd_pcapwalk.hip): one chunk of capture bytes in HBM.

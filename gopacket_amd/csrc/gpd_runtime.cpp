@@ -628,10 +628,8 @@ static int launch(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, hipS
     Q.csum = out->csum ? out->csum + lo : nullptr;
     Q.ext = out->ext ? out->ext + lo : nullptr;
     Q.hdr_off = out->hdr_off ? out->hdr_off + lo : nullptr;
-    if (gpd::fast_eligible(P)) {  // two counters in their own lines, used alternately: each
-      auto &fb = ctx->fallback[stream];  // list kernel zeroes the one the next launch takes
-      Q.fb_count = fb.d + 64 * fb.parity;
-      Q.fb_next = fb.d + 64 * (fb.parity ^ 1u);
+    if (gpd::fast_eligible(P)) {  // per-wave counts, two arrays used alternately (a timed
+      auto &fb = ctx->fallback[stream];  // launch's counts survive the next launch for the split)
       Q.fb_wcount = fb.wc + (size_t)ctx->num_cus * gpd::kMaxFastWavesPerCU * fb.parity;
       fb.parity ^= 1u;
     }

@@ -355,7 +355,7 @@ def make_tcp64(n: int, seed: int = 0x5EED0008, chunk: int = 1 << 18) -> PacketBa
 MIX_CLASSES = (("tcp64", 64, 30), ("tcp576", 576, 15), ("tcp1500", 1500, 8), ("udp64", 64, 20),
                ("vxlan", 128, 5), ("icmp4", 98, 5), ("tcp6", 86, 5), ("stp", 60, 1),
                ("ip4opt", 68, 4), ("frag", 64, 3), ("ip6hbh", 90, 2), ("tcpcut", 64, 2))
-MIX_FALLBACK = ("stp", "ip4opt", "frag", "ip6hbh", "tcpcut")
+MIX_FALLBACK = ("stp", "ip4opt", "ip6hbh", "tcpcut")  # (IPv4 fragments: the fast path, r03)
 
 
 def _mix_class(name: str, m: int, seed: int, free_t, free_u) -> np.ndarray:
@@ -441,9 +441,9 @@ def _mix_class(name: str, m: int, seed: int, free_t, free_u) -> np.ndarray:
 
 def make_traffic_mix(n: int, seed: int = 0x5EED0007, align: int = 16) -> PacketBatch:
     """A seeded mix of MIX_CLASSES by weight, shuffled: TCP 64/576/1500, UDP 64, VXLAN, ICMPv4
-    echo and IPv6/TCP frames that the fast kernel decodes, plus 802.3/LLC frames, IPv4 options,
-    IPv4 fragments, IPv6 hop-by-hop and cut TCP headers (12 %, MIX_FALLBACK) that it leaves to
-    the generic decoder.  Checksums are valid except 1 in 64 TCP frames."""
+    echo, IPv6/TCP and IPv4 fragments that the fast kernel decodes, plus 802.3/LLC frames, IPv4
+    options, IPv6 hop-by-hop and cut TCP headers (MIX_FALLBACK, 9 %) that it leaves to the
+    generic decoder.  Checksums are valid except 1 in 64 TCP frames."""
     wsum = sum(w for _, _, w in MIX_CLASSES)
     counts = [n * w // wsum for _, _, w in MIX_CLASSES]
     counts[0] += n - sum(counts)

@@ -349,9 +349,10 @@ int  gpd_sync(gpd_ctx *ctx, void *stream);
 int  gpd_ctx_set_timing(gpd_ctx *ctx, int enable);
 float gpd_last_kernel_ms(gpd_ctx *ctx);
 /* The last timed gpd_decode split in two (synchronises its stream): the packets the fast
- * kernel left to the generic decoder (options, fragments, hop-by-hop, errors, ...), the fast
- * kernel's time and the generic list kernel's time (ms).  Needs a timed launch that took the
- * fast path (Ethernet first, hashed tables, no ext records). */
+ * decode left to the generic decoder (options, fragments, hop-by-hop, errors, ...), the fast
+ * kernel's time (each of its waves decodes its own fallback list at its end, so that time
+ * includes the generic decodes) and the time after it to the end of the call (ms, ~0).  Needs a
+ * timed launch that took the fast path (Ethernet first, hashed tables, no ext records). */
 int  gpd_last_launch_split(gpd_ctx *ctx, uint64_t *fallback, float *fast_ms, float *list_ms);
 
 /* Engine tuning of later launches on ctx.  None of these changes a result — every setting

@@ -402,10 +402,11 @@ def test_traffic_mix_both_kernels(mask):
 
 
 def test_fallback_split_counts_the_generic_share():
-    """gpd_last_launch_split: the fast kernel decodes ICMPv4, LLC, IPv6/TCP and VXLAN itself,
-    and leaves exactly the IPv4-options, fragment, hop-by-hop and cut-TCP frames to the list
-    kernel — with header-once off.  With header-once on (the mix's long frames choose it), a
-    wave's few VXLAN frames go to the list kernel too, and the results stay exact."""
+    """gpd_last_launch_split: the fast decode takes ICMPv4, IPv6/TCP and VXLAN itself, and
+    leaves exactly the IPv4-options, fragment, hop-by-hop, LLC and cut-TCP frames to the generic
+    decoder (each wave's fallback list, decoded at the end of that wave) — with header-once off.
+    With header-once on (the mix's long frames choose it), a wave's few VXLAN frames fall back
+    too, and the results stay exact."""
     import ctypes as C
     from gopacket_amd import parser as P
     from gopacket_amd._lib import check, lib
@@ -429,7 +430,7 @@ def test_fallback_split_counts_the_generic_share():
             assert fb.value == want
         else:
             assert want < fb.value <= want + n_vx
-        assert f.value > 0 and l.value > 0
+        assert f.value > 0 and l.value >= 0  # (the lists are decoded inside the fast kernel)
         res = dr.to_host()
         for k in ("status", "layers", "net_hash", "tp_hash", "csum", "hdr_off"):
             assert np.array_equal(getattr(res, k), getattr(ref, k)), k

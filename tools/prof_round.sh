@@ -21,3 +21,7 @@ run kt --kernel-trace --stats &&
 run fetch --pmc FETCH_SIZE &&
 run write --pmc WRITE_SIZE &&
 run sq --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY
+# optional LDS pass (PROF_LDS=1): bank conflicts and LDS-array cycles of the decode kernel
+if [ "${PROF_LDS:-0}" = 1 ]; then
+  run lds --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES
+fi

@@ -60,6 +60,9 @@ def summarize(d):
         s["hbm_write_bytes_per_launch"] = write["WRITE_SIZE"] * 1024
     if sq:
         s["sq_per_launch"] = sq
+    lds, _ = counters(d, "lds")
+    if lds:
+        s["lds_per_launch"] = lds
     return s
 
 

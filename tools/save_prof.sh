@@ -8,7 +8,7 @@ D=profiles/$R/$CFG
 mkdir -p "$D"
 python3 tools/prof_summary.py "$SRC" > "$D/summary.json"
 cp "$(find "$SRC/kt" -name '*kernel_stats.csv' | head -1)" "$D/kt_kernel_stats.csv"
-for p in fetch write sq; do
+for p in fetch write sq lds; do
   f=$(find "$SRC/$p" -name '*counter_collection.csv' 2>/dev/null | head -1)
   [ -n "$f" ] && cp "$f" "$D/pmc_${p}_counter_collection.csv"
 done
