@@ -268,6 +268,31 @@ def bench_record36(parser, dev_batch, n, local, stream, out, args, records=False
             "read_frac": round(rb / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
+def attainable(n: int, read_bytes: int, local: int, achieved_gbps: float):
+    """The streaming ceiling for this launch's traffic shape on this box (libgpd_probe.so): the
+    same read bytes per 64-packet tile as one contiguous run and the same 2 KiB of records per
+    tile, no decode, no packet boundaries, after its own clock settle.  `frac` of the decode is
+    read against peak; `of_attainable` against this.  None without the probe."""
+    import ctypes as C
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gopacket_amd", "libgpd_probe.so")
+    if not os.path.exists(path):
+        return None
+    lib = C.CDLL(path)
+    lib.gpd_probe_stream.argtypes = [C.c_int, C.c_uint32, C.c_uint32, C.c_int, C.c_float, C.POINTER(C.c_float)]
+    ntiles = (n + 63) // 64
+    per_tile = -(-read_bytes // ntiles)
+    ms = C.c_float(0.0)
+    rc = lib.gpd_probe_stream(local, ntiles, per_tile, 20, 150.0, C.byref(ms))
+    if rc != 0 or ms.value <= 0:
+        return {"error": f"gpd_probe_stream rc={rc}"}
+    gbps = (ntiles * per_tile + ntiles * 2048) / (ms.value * 1e-3) / 1e9
+    return {"GBps": round(gbps, 1), "frac_of_peak": round(gbps / HBM_PEAK_GBS, 4),
+            "of_attainable": round(achieved_gbps / gbps, 4), "probe_ms": round(ms.value, 4),
+            "read_bytes_per_tile": per_tile, "write_bytes_per_tile": 2048,
+            "probe": "gpd_probe_stream: contiguous 16-B-per-lane nt loads of each tile's read bytes + "
+                     "two 16-B nt record stores per lane, no decode (2 and 4 workgroups per CU, best)"}
+
+
 SIDE_CONFIGS = ("tcp64", "imix", "vxlan", "pcap64")  # timed beside the default line (N = 1)
 
 
@@ -314,6 +339,8 @@ def bench_side(config, parser, args, local, stream):
            "algorithmic_read_bytes": read, "algorithmic_write_bytes": write,
            "decode_errors_in_batch": int(np.count_nonzero((st & 3) != 0)),
            "settle_ms": settled, "generate_s": round(t_gen, 2)}
+    if not args.no_probe:
+        out["attainable"] = attainable(n, read, local, out["achieved_GBps"])
     tr = load_traffic(config)
     if tr and tr["read"] and tr["write"]:
         out["traffic"] = int(tr["read"]) + int(tr["write"])
@@ -1018,6 +1045,8 @@ def main():
                     help="tests only: gloo rehearses the N-rank path without RCCL")
     ap.add_argument("--same-device", action="store_true",
                     help="tests only: every rank on cuda:0 (the N-rank path on a one-GPU box, gloo)")
+    ap.add_argument("--no-probe", action="store_true", help="skip the attainable-bandwidth probe "
+                    "(roofline.attainable)")
     ap.add_argument("--lean", action="store_true", help="only the timed launches (profiling runs: "
                     "no 36-B record line, no fallback split, no CPU baseline)")
     args = ap.parse_args()
@@ -1177,6 +1206,9 @@ def main():
         if world == 1 and batch is not None and not pcap_info:
             # the same batch from host memory (north star: the rate including pinned H2D/D2H)
             out["pcie_inclusive"] = bench_host(parser, batch, n, "registered", 3, 1)
+    if not args.ablate and not args.lean and not args.no_probe:
+        rf = out["roofline"]
+        rf["attainable"] = attainable(n, rf["algorithmic_read_bytes"], local, rf["achieved"])
     if pcap_info:
         out["pcap"] = pcap_info
         if args.replay:

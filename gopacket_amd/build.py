@@ -4,6 +4,7 @@
   oracle/libgpd_oracle.so      test infrastructure: CPU restatement (oracle/)
   tests/c/abi_host             test driver: a plain C host on the C-ABI (no Python/torch)
   gopacket_amd/libgpd_synth.so workload generator for the bench (config 5 captures); not product
+  gopacket_amd/libgpd_probe.so attainable-bandwidth probe bench.py prints beside each roofline; not product
 
 Both are built with plain compiler invocations (hipcc / gcc); no cmake.  The .so
 files are git-ignored and travel to the GPU box with the repository snapshot.
@@ -75,6 +76,19 @@ def build_synth(force: bool = False) -> str:
     return SYNTH_LIB
 
 
+PROBE_LIB = os.path.join(PKG, "libgpd_probe.so")
+
+
+def build_probe(force: bool = False) -> str:
+    """gopacket_amd/libgpd_probe.so: the streaming probe of bench.py's `roofline.attainable`."""
+    src = os.path.join(CSRC, "gpd_probe.hip")
+    if force or _stale(PROBE_LIB, [src]):
+        subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
+                        src, "-o", PROBE_LIB + ".tmp"], check=True)
+        os.replace(PROBE_LIB + ".tmp", PROBE_LIB)
+    return PROBE_LIB
+
+
 def build_abi_host(force: bool = False) -> str:
     """tests/c/abi_host: links libgpd.so (rpath to the in-tree copy) and the oracle."""
     src = os.path.join(ROOT, "tests", "c", "abi_host.c")
@@ -95,3 +109,4 @@ if __name__ == "__main__":
     print(build_oracle(force=force))
     print(build_abi_host(force=force))
     print(build_synth(force=force))
+    print(build_probe(force=force))

@@ -1,0 +1,107 @@
+// gpd_probe.hip — the attainable-bandwidth probe printed beside each roofline in bench.py.
+//
+// Diagnostic only (libgpd_probe.so, not part of the C-ABI in include/): how fast does plain
+// register-staged streaming move the SAME traffic shape as a decode launch on this box — per
+// 64-packet tile, the tile's algorithmic read bytes (packet bytes + descriptors) as one
+// contiguous run loaded 16 B per lane, and its 64 x 32-B result records written as two
+// 16-B nontemporal stores per lane — with no decode and no packet boundaries?  A decode
+// kernel's `frac` against HBM peak reads against this figure: the gap between the two is the
+// decode's and the window planner's cost, the gap between this and 1.0 is the part's.
+// (tools/micro/hbm_mix.hip is the sweep this was taken from; its "mix72/32" row.)
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace {
+
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+
+constexpr uint32_t kMaxTileBytes = 1u << 20;  // read bytes per tile accepted
+
+// One wave per 64-packet tile (grid stride).  ctile: the tile's 16-B read chunks; lane l loads
+// chunks l, l + 64, ... of the tile, MAXC per lane in flight together (rounds of them for long
+// tiles), folds them, then stores the tile's records.
+template <int MAXC>
+__global__ __launch_bounds__(256) void probe_k(const v4u *__restrict__ in, v4u *__restrict__ rec,
+                                               uint32_t ntiles, uint32_t ctile) {
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint32_t nw = gridDim.x * 4u;
+  for (uint32_t t = blockIdx.x * 4u + wave; t < ntiles; t += nw) {
+    const v4u *p = in + (uint64_t)t * ctile;
+    uint32_t x = 0;
+    for (uint32_t c0 = 0; c0 < ctile; c0 += 64u * MAXC) {
+      v4u v[MAXC];
+#pragma unroll
+      for (int j = 0; j < MAXC; j++) {
+        const uint32_t c = c0 + 64u * j + lane;
+        v[j] = c < ctile ? __builtin_nontemporal_load(p + c) : v4u{0u, 0u, 0u, 0u};
+      }
+#pragma unroll
+      for (int j = 0; j < MAXC; j++) x ^= v[j].x + v[j].y + v[j].z + v[j].w;
+    }
+    const uint64_t i = (uint64_t)t * 64u + lane;
+    __builtin_nontemporal_store(v4u{x, x ^ 1u, x * 3u, 0u}, rec + 2 * i);
+    __builtin_nontemporal_store(v4u{x * 5u, 0u, x * 7u, 0u}, rec + 2 * i + 1);
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// Streams ntiles tiles of read_bytes_per_tile (rounded up to 16, at most 1 MiB) and 2 KiB of
+// records each, at 2 and 4 workgroups per CU, `reps` timed launches after `warm_ms` of untimed
+// ones; *best_ms is the fastest configuration's mean launch time.  0 on success, else the HIP
+// error code.  Allocates and frees its own buffers.
+int gpd_probe_stream(int device, uint32_t ntiles, uint32_t read_bytes_per_tile, int reps, float warm_ms,
+                     float *best_ms) {
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return (int)e;
+  const uint32_t ctile = (read_bytes_per_tile + 15u) / 16u;
+  if (ctile == 0 || ctile > kMaxTileBytes / 16u || ntiles == 0 || reps <= 0) return (int)hipErrorInvalidValue;
+  hipDeviceProp_t prop;
+  if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) return (int)e;
+  v4u *in = nullptr, *rec = nullptr;
+  hipEvent_t a = nullptr, b = nullptr;
+  float best = 0.0f;
+  if ((e = hipMalloc(&in, (size_t)ntiles * ctile * 16u)) != hipSuccess) goto done;
+  if ((e = hipMalloc(&rec, (size_t)ntiles * 2048u)) != hipSuccess) goto done;
+  if ((e = hipMemset(in, 0x5a, (size_t)ntiles * ctile * 16u)) != hipSuccess) goto done;
+  if ((e = hipEventCreate(&a)) != hipSuccess || (e = hipEventCreate(&b)) != hipSuccess) goto done;
+  for (int wpc : {2, 4}) {
+    const uint32_t g = (uint32_t)prop.multiProcessorCount * (uint32_t)wpc;
+    const uint32_t pl = (ctile + 63u) / 64u;  // chunks per lane per tile
+    auto launch = [&] {  // a 64-B-frame tile (4.5 KiB) in one round; longer tiles in rounds of 8 KiB
+      if (pl <= 5u) hipLaunchKernelGGL(probe_k<5>, dim3(g), dim3(256), 0, 0, in, rec, ntiles, ctile);
+      else hipLaunchKernelGGL(probe_k<8>, dim3(g), dim3(256), 0, 0, in, rec, ntiles, ctile);
+    };
+    // untimed launches for warm_ms (the clocks settle, as bench.py does for the decode)
+    float spent = 0.0f;
+    while (spent < warm_ms) {
+      if ((e = hipEventRecord(a, 0)) != hipSuccess) goto done;
+      for (int r = 0; r < 10; r++) launch();
+      if ((e = hipEventRecord(b, 0)) != hipSuccess || (e = hipEventSynchronize(b)) != hipSuccess) goto done;
+      float ms = 0.0f;
+      if ((e = hipEventElapsedTime(&ms, a, b)) != hipSuccess) goto done;
+      spent += ms;
+      if (ms <= 0.0f) break;
+    }
+    if ((e = hipEventRecord(a, 0)) != hipSuccess) goto done;
+    for (int r = 0; r < reps; r++) launch();
+    if ((e = hipEventRecord(b, 0)) != hipSuccess || (e = hipEventSynchronize(b)) != hipSuccess) goto done;
+    float ms = 0.0f;
+    if ((e = hipEventElapsedTime(&ms, a, b)) != hipSuccess) goto done;
+    ms /= (float)reps;
+    if ((e = hipGetLastError()) != hipSuccess) goto done;
+    if (best == 0.0f || ms < best) best = ms;
+  }
+  *best_ms = best;
+done:
+  if (a) (void)hipEventDestroy(a);
+  if (b) (void)hipEventDestroy(b);
+  if (in) (void)hipFree(in);
+  if (rec) (void)hipFree(rec);
+  return (int)e;
+}
+
+}  // extern "C"
