@@ -21,9 +21,10 @@ constexpr uint32_t kMaxTileBytes = 1u << 20;  // read bytes per tile accepted
 // One wave per 64-packet tile (grid stride).  ctile: the tile's 16-B read chunks; lane l loads
 // chunks l, l + 64, ... of the tile, MAXC per lane in flight together (rounds of them for long
 // tiles), folds them, then stores the tile's records.
-template <int MAXC>
+template <int MAXC, bool COMMIT = false>
 __global__ __launch_bounds__(256) void probe_k(const v4u *__restrict__ in, v4u *__restrict__ rec,
                                                uint32_t ntiles, uint32_t ctile) {
+  extern __shared__ v4u lds[];  // COMMIT: each round's chunks are copied to the wave's LDS first
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const uint32_t nw = gridDim.x * 4u;
   for (uint32_t t = blockIdx.x * 4u + wave; t < ntiles; t += nw) {
@@ -35,6 +36,13 @@ __global__ __launch_bounds__(256) void probe_k(const v4u *__restrict__ in, v4u *
       for (int j = 0; j < MAXC; j++) {
         const uint32_t c = c0 + 64u * j + lane;
         v[j] = c < ctile ? __builtin_nontemporal_load(p + c) : v4u{0u, 0u, 0u, 0u};
+      }
+      if (COMMIT) {
+#pragma unroll
+        for (int j = 0; j < MAXC; j++) lds[(wave * MAXC + j) * 64 + lane] = v[j];
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        const v4u q = lds[(wave * MAXC) * 64 + ((lane * 5 + 3) & 63)];
+        x ^= q.x + q.y;
       }
 #pragma unroll
       for (int j = 0; j < MAXC; j++) x ^= v[j].x + v[j].y + v[j].z + v[j].w;
@@ -96,6 +104,54 @@ int gpd_probe_stream(int device, uint32_t ntiles, uint32_t read_bytes_per_tile, 
     if (best == 0.0f || ms < best) best = ms;
   }
   *best_ms = best;
+done:
+  if (a) (void)hipEventDestroy(a);
+  if (b) (void)hipEventDestroy(b);
+  if (in) (void)hipFree(in);
+  if (rec) (void)hipFree(rec);
+  return (int)e;
+}
+
+// Diagnostics of the streaming structure (tools/): the same probe at a given
+// number of workgroups per CU (wpc), with lds_per_wg bytes of dynamic LDS per workgroup (to cap
+// the resident waves as a decode kernel's LDS does) and optionally every round copied to LDS
+// before it is folded (commit).  *ms: mean launch time after warm_ms of untimed launches.
+int gpd_probe_stream_ex(int device, uint32_t ntiles, uint32_t read_bytes_per_tile, int reps, float warm_ms,
+                        uint32_t wpc, uint32_t lds_per_wg, int commit, float *ms_out) {
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return (int)e;
+  const uint32_t ctile = (read_bytes_per_tile + 15u) / 16u;
+  if (ctile == 0 || ctile > kMaxTileBytes / 16u || ntiles == 0 || reps <= 0 || wpc == 0) return (int)hipErrorInvalidValue;
+  hipDeviceProp_t prop;
+  if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) return (int)e;
+  const uint32_t need = commit ? 4u * 8u * 64u * 16u : 0u;  // 4 waves x 8 chunks x 64 lanes
+  const uint32_t lds = lds_per_wg > need ? lds_per_wg : need;
+  v4u *in = nullptr, *rec = nullptr;
+  hipEvent_t a = nullptr, b = nullptr;
+  float ms = 0.0f, spent = 0.0f;
+  const uint32_t g = (uint32_t)prop.multiProcessorCount * wpc;
+  auto launch = [&] {
+    if (commit) hipLaunchKernelGGL((probe_k<8, true>), dim3(g), dim3(256), lds, 0, in, rec, ntiles, ctile);
+    else hipLaunchKernelGGL((probe_k<8, false>), dim3(g), dim3(256), lds, 0, in, rec, ntiles, ctile);
+  };
+  if ((e = hipMalloc(&in, (size_t)ntiles * ctile * 16u)) != hipSuccess) goto done;
+  if ((e = hipMalloc(&rec, (size_t)ntiles * 2048u)) != hipSuccess) goto done;
+  if ((e = hipMemset(in, 0x5a, (size_t)ntiles * ctile * 16u)) != hipSuccess) goto done;
+  if ((e = hipEventCreate(&a)) != hipSuccess || (e = hipEventCreate(&b)) != hipSuccess) goto done;
+  while (spent < warm_ms) {
+    if ((e = hipEventRecord(a, 0)) != hipSuccess) goto done;
+    for (int r = 0; r < 10; r++) launch();
+    if ((e = hipEventRecord(b, 0)) != hipSuccess || (e = hipEventSynchronize(b)) != hipSuccess) goto done;
+    if ((e = hipEventElapsedTime(&ms, a, b)) != hipSuccess) goto done;
+    spent += ms;
+    if (ms <= 0.0f) break;
+  }
+  if ((e = hipEventRecord(a, 0)) != hipSuccess) goto done;
+  for (int r = 0; r < reps; r++) launch();
+  if ((e = hipEventRecord(b, 0)) != hipSuccess || (e = hipEventSynchronize(b)) != hipSuccess) goto done;
+  if ((e = hipEventElapsedTime(&ms, a, b)) != hipSuccess) goto done;
+  if ((e = hipGetLastError()) != hipSuccess) goto done;
+  *ms_out = ms / (float)reps;
 done:
   if (a) (void)hipEventDestroy(a);
   if (b) (void)hipEventDestroy(b);
