@@ -224,6 +224,30 @@ def test_header_once_both_ways(ho, extra):
     run_both(NP.index(cap).batch, ext=False, tuning=t)
 
 
+def test_header_once_tile_shapes():
+    """The header-once kernel over batch shapes that stress its tiles and windows: 1..200
+    packets (fewer tiles than waves, a partial last tile), tiles in reverse and shuffled order,
+    frames larger than a window between small ones, and a long IMIX batch."""
+    t = dict(window_bytes=8192, header_once=1)
+    base = synth.make_imix(1 << 12, seed=0x5EED0401)
+    pk = [base.packet(i) for i in range(base.n)]
+    for m in (1, 63, 64, 65, 130, 200):
+        run_both(PacketBatch.from_packets(pk[:m]), ext=False, tuning=t)
+    b = PacketBatch.from_packets(pk)
+    for order in (np.arange(b.n)[::-1].copy(), np.random.default_rng(4).permutation(b.n),
+                  np.concatenate([np.arange(64 * k, 64 * k + 64)[::-1] for k in range(b.n // 64)])):
+        run_both(PacketBatch(b.data, b.data_len, b.offset[order].copy(), b.caplen[order].copy()),
+                 ext=False, tuning=t)
+    big = [G.case_bytes(c) for c in CASES if c["name"] == "ipv6_jumbogram_dlp"][0]
+    mixed = []
+    for i, p in enumerate(pk[:1500]):
+        mixed.append(p)
+        if i % 97 == 5:
+            mixed.append(big + big[:3000])
+    run_both(PacketBatch.from_packets(mixed), ext=False, tuning=t)
+    run_both(synth.make_imix(1 << 17, seed=0x5EED0402), ext=False, tuning=t)
+
+
 def test_layouts_unaligned_shuffled_large_empty():
     pk = _golden_packets() + [b"", b"\x01", b"\x00" * 13]
     big = [G.case_bytes(c) for c in CASES if c["name"] == "ipv6_jumbogram_dlp"][0]
