@@ -121,6 +121,30 @@ struct GlbSrc {
   }
 };
 
+// A fallback packet whose first K bytes (from its 16-aligned global start) a lane staged in
+// its own LDS slot: reads below that bound come from LDS, the rest (long segments' checksums)
+// from global memory.  The generic decoder's chain of dependent header reads then costs LDS
+// latency instead of HBM latency (rs_kernel's end-of-wave fallback lists).
+template <uint32_t K>
+struct HybSrc {
+  const uint8_t *data;
+  uint64_t pos;    // global offset of the packet's first byte
+  uint64_t gbase;  // pos & ~15: global offset of slot byte 0
+  uint32_t slot;   // LDS address of the lane's slot
+  __device__ __forceinline__ uint64_t abs(uint32_t rel) const { return pos + rel; }
+  __device__ __forceinline__ uint32_t dw(uint64_t a) const {
+    return a - gbase < K ? lds_u32(slot + (uint32_t)(a - gbase)) : *reinterpret_cast<const uint32_t *>(data + a);
+  }
+  __device__ __forceinline__ uint32_t u8(uint32_t rel) const {
+    const uint64_t a = pos + rel;
+    return a - gbase < K ? (uint32_t)g_lds[slot + (uint32_t)(a - gbase)] : (uint32_t)data[a];
+  }
+  __device__ __forceinline__ uint4 q(uint64_t a) const {
+    return a - gbase < K ? *reinterpret_cast<const uint4 *>(g_lds + slot + (uint32_t)(a - gbase))
+                         : *reinterpret_cast<const uint4 *>(data + a);
+  }
+};
+
 // N little-endian words holding packet bytes [rel, rel+4N) (unaligned start).
 template <int N, class S>
 __device__ __forceinline__ void load_words(const S &s, uint32_t rel, uint32_t (&w)[N]) {
@@ -2026,15 +2050,35 @@ __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
   // with the other waves' streaming.  (A second kernel over the lists cost a launch boundary,
   // ~5 us per launch, even when every list is empty.)  The live state of the loop above is dead
   // by now, so the generic decoder's registers do not raise the kernel's.
+  // Each round first stages every listed packet's first STAGE/64 bytes in the lane's slot of the
+  // (now idle) window buffer with independent 16-byte loads, so the decoder's dependent header
+  // reads hit LDS (HybSrc); bytes past the slot (long segments) still come from global memory.
   if (!(kExp & 8u) && fb_c) {
     __threadfence_block();  // the entries other lanes of this wave stored
     const Tab<false> T{P.pages,    P.eth_base, P.tcp_base, P.udp_base, P.eth_bits,
                        P.tcp_bits, P.udp_bits, P.eth_mult, P.tcp_mult, P.udp_mult};
-    for (uint32_t j = lane; j < fb_c; j += 64u) {
-      const uint32_t fi = P.fb_list[fb_start + j];
-      const uint32_t off = min(P.offset[fi], dlen);
-      const uint32_t len = min(P.caplen[fi], dlen - off);
-      store_out(P, fi, decode_packet<false>(GlbSrc{P.data, off}, len, T, P.first, options, nullptr));
+    constexpr uint32_t K = (uint32_t)STAGE / 64u;
+    const uint32_t slot = buf + K * lane;
+    const uint64_t rlim = (((uint64_t)dlen + 15u) & ~15ull) + 16u;  // readable (batch contract)
+    for (uint32_t j = lane; j - lane < fb_c; j += 64u) {
+      const bool live = j < fb_c;
+      const uint32_t fi = live ? P.fb_list[fb_start + j] : 0u;
+      const uint32_t off = live ? min(P.offset[fi], dlen) : 0u;
+      const uint32_t len = live ? min(P.caplen[fi], dlen - off) : 0u;
+      const uint64_t gb = (uint64_t)off & ~15ull;
+      if (!(kExp & 128u)) {
+        v4u32 c[K / 16u];
+#pragma unroll
+        for (uint32_t k = 0; k < K / 16u; k++)
+          c[k] = (live && gb + 16u * k < rlim) ? *reinterpret_cast<const v4u32 *>(P.data + gb + 16u * k)
+                                                : v4u32{0u, 0u, 0u, 0u};
+#pragma unroll
+        for (uint32_t k = 0; k < K / 16u; k++) *reinterpret_cast<v4u32 *>(g_lds + slot + 16u * k) = c[k];
+        if (live)
+          store_out(P, fi, decode_packet<false>(HybSrc<K>{P.data, off, gb, slot}, len, T, P.first, options, nullptr));
+      } else if (live) {
+        store_out(P, fi, decode_packet<false>(GlbSrc{P.data, off}, len, T, P.first, options, nullptr));
+      }
     }
   }
 }
