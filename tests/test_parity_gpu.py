@@ -248,6 +248,65 @@ def test_header_once_tile_shapes():
     run_both(synth.make_imix(1 << 17, seed=0x5EED0402), ext=False, tuning=t)
 
 
+def _ip4_option_frames(n, seed):
+    """Long TCP and UDP frames whose IPv4 headers carry 1..10 option words: valid walks (NOP,
+    EOL + padding, Router Alert, record-route-like TLVs) and each ip4.go:240-273 error (length
+    byte 0 / 1 / 2, a TLV past the header, a type byte alone at the end), some with IHL*4 beyond
+    Length or the capture, checksums sometimes right."""
+    rng = np.random.default_rng(seed)
+    base = synth.make_imix(n, seed=seed)
+    out = []
+    for i in range(n):
+        p = bytearray(base.packet(i))
+        eth = 18 if p[12:14] == b"\x81\x00" else 14
+        if len(p) < eth + 40:
+            out.append(bytes(p))
+            continue
+        k = int(rng.integers(1, 11))
+        opts = bytearray()
+        while len(opts) < 4 * k:
+            r = rng.random()
+            room = 4 * k - len(opts)
+            if r < 0.3:
+                opts.append(1)
+            elif r < 0.4:
+                opts += b"\x00" + bytes(room - 1)
+            elif r < 0.75 and room >= 3:
+                ln = int(rng.integers(3, room + 1))
+                opts += bytes([int(rng.integers(2, 255)), ln]) + bytes(rng.integers(0, 256, ln - 2, dtype=np.uint8))
+            else:  # an error
+                e = int(rng.integers(0, 4))
+                if e == 0 and room >= 2:
+                    opts += bytes([7, int(rng.integers(0, 3))])
+                elif e == 1 and room >= 2:
+                    opts += bytes([7, room + int(rng.integers(1, 9))])
+                else:
+                    opts += bytes([int(rng.integers(2, 255))])
+        opts = opts[:4 * k]
+        hdr = p[eth:eth + 20]
+        hdr[0] = 0x40 | (5 + k)
+        total = int.from_bytes(hdr[2:4], "big") + 4 * k
+        if rng.random() < 0.1:
+            total = 20 + int(rng.integers(0, 4 * k))
+        hdr[2:4] = (total & 0xFFFF).to_bytes(2, "big")
+        q = p[:eth] + hdr + opts + p[eth + 20:]
+        if rng.random() < 0.05:
+            q = q[:eth + 20 + int(rng.integers(0, 4 * k))]
+        out.append(bytes(q))
+    return out
+
+
+@pytest.mark.parametrize("ho", [0, 1])
+def test_ip4_options_both_ways(ho):
+    """IPv4 options on long frames: the header-once kernel walks them in seg_pass (ip4_options)
+    and decodes the packets in its straight-line pass; the per-window kernel leaves them to the
+    generic decoder.  Both against the oracle, valid and erroneous options alike."""
+    t = dict(window_bytes=8192, header_once=ho)
+    run_both(PacketBatch.from_packets(_ip4_option_frames(1 << 12, 0x5EED0501)), ext=False, tuning=t)
+    pk = _ip4_option_frames(1 << 11, 0x5EED0502)
+    run_both(PacketBatch.from_packets(pk, align=1), ext=False, tuning=t)
+
+
 def test_layouts_unaligned_shuffled_large_empty():
     pk = _golden_packets() + [b"", b"\x01", b"\x00" * 13]
     big = [G.case_bytes(c) for c in CASES if c["name"] == "ipv6_jumbogram_dlp"][0]
