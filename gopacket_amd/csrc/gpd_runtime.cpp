@@ -538,7 +538,7 @@ static int check_batch(const gpd_batch *in, const gpd_result *out) {
 // n_dev: the packet count is read on the device (at most in->n); geom_n: the packet count the
 // staging choices assume (0: in->n) — both for batches whose records the device walk found.
 static int launch(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, hipStream_t stream,
-                  bool record, const uint32_t *n_dev = nullptr, uint64_t geom_n = 0) {
+                  bool record, const uint32_t *n_dev = nullptr, uint64_t geom_n = 0, uint64_t geom_bytes = 0) {
   gpd::KParams P{};
   P.data = in->data;
   P.data_len = in->data_len;
@@ -564,7 +564,7 @@ static int launch(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, hipS
   P.fixed = ctx->fixed;
   // LDS window per buffer: the smallest of 4/8 KiB that holds a typical 64-packet tile
   const uint64_t gn = geom_n ? geom_n : in->n;
-  const uint64_t mean_slot = (in->data_len + gn - 1) / gn;
+  const uint64_t mean_slot = ((geom_bytes ? geom_bytes : in->data_len) + gn - 1) / gn;
   P.stage = mean_slot * 64 <= 4096 ? 4096u : 8192u;
   if (ctx->tune.window_bytes) P.stage = ctx->tune.window_bytes;
   P.first = ctx->first;
@@ -855,13 +855,20 @@ int gpd_decode_host(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out) {
     const bool reg = j > i && ctx->is_registered(in->data + lo16, span_hi - lo16);
     const bool span = j > i && (span_hi - lo16) <= (reg ? 4 : 2) * used + 4096;
     uint64_t pos = 0;
+    // a span whose descriptors are registered too (a capture loop pins its arrays once): they
+    // travel by DMA as they are, and the kernel reads the window through a base pointer moved
+    // back by lo16, so the caller's absolute offsets index it — no host pass over the chunk
+    bool dreg = false;
     if (span) {
       pos = span_hi - lo16;
       const uint64_t m = j - i;
-      par_for(m, 1u << 16, [&](uint64_t a, uint64_t b) {
-        for (uint64_t p = a; p < b; p++) s.h_off[p] = (uint32_t)(in->offset[i + p] - lo16);
-        std::memcpy(s.h_len + a, in->caplen + i + a, (b - a) * 4);
-      });
+      dreg = ctx->is_registered((const uint8_t *)(in->offset + i), m * 4) &&
+             ctx->is_registered((const uint8_t *)(in->caplen + i), m * 4);
+      if (!dreg)
+        par_for(m, 1u << 16, [&](uint64_t a, uint64_t b) {
+          for (uint64_t p = a; p < b; p++) s.h_off[p] = (uint32_t)(in->offset[i + p] - lo16);
+          std::memcpy(s.h_len + a, in->caplen + i + a, (b - a) * 4);
+        });
       const uint64_t bytes = std::min<uint64_t>((pos + 15) & ~15ull, ((in->data_len + 15) & ~15ull) - lo16);
       if (ctx->is_registered(in->data + lo16, bytes)) {
         HIP_TRY(hipMemcpyAsync(s.d_data, in->data + lo16, bytes, hipMemcpyHostToDevice, s.stream));
@@ -894,12 +901,16 @@ int gpd_decode_host(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out) {
       HIP_TRY(hipMemcpyAsync(s.d_data, s.h_data, (pos + 15) & ~15ull, hipMemcpyHostToDevice, s.stream));
     }
     const uint64_t m = j - i;
-    HIP_TRY(hipMemcpyAsync(s.d_off, s.h_off, m * 4, hipMemcpyHostToDevice, s.stream));
-    HIP_TRY(hipMemcpyAsync(s.d_len, s.h_len, m * 4, hipMemcpyHostToDevice, s.stream));
+    HIP_TRY(hipMemcpyAsync(s.d_off, dreg ? in->offset + i : s.h_off, m * 4, hipMemcpyHostToDevice, s.stream));
+    HIP_TRY(hipMemcpyAsync(s.d_len, dreg ? in->caplen + i : s.h_len, m * 4, hipMemcpyHostToDevice, s.stream));
     gpd_batch b{s.d_data, pos, s.d_off, s.d_len, m};
+    if (dreg) {
+      b.data = s.d_data - lo16;  // 16-aligned (lo16 is); the kernel never reads below lo16
+      b.data_len = lo16 + pos;
+    }
     gpd_result r{s.d_status, s.d_layers, s.d_nh, s.d_th, s.d_csum, out->ext ? s.d_ext : nullptr,
                  out->hdr_off ? s.d_hoff : nullptr};
-    rc = launch(ctx, &b, &r, s.stream, false);
+    rc = launch(ctx, &b, &r, s.stream, false, nullptr, 0, pos);
     if (rc) return rc;
     HIP_TRY(results_d2h(ctx, s, out, i, m));
     s.lo = i;

@@ -365,6 +365,30 @@ def test_host_path_matches_device_path():
     assert_same(p.DecodeBatchHost(sparse, ext=False), p.DecodeBatch(sparse, ext=False), sparse, ext=False)
 
 
+def test_host_path_with_registered_descriptors():
+    """Span chunks whose offset and caplen arrays are registered too travel without a host pass:
+    the descriptors by DMA as they are, the window read through a base pointer moved back by the
+    chunk's start.  Several 2^20-packet chunks (chunk starts far from 0), a batch starting past
+    byte 0, and the tail chunk, against the device path."""
+    from gopacket_amd import parser as P
+    from gopacket_amd._lib import check, lib
+    u = synth.make_udp64((1 << 21) + 12345)
+    m = synth.make_mixed(3000)
+    p = P.DecodingLayerParser(L.LayerTypeEthernet)
+    p._mask = ALL
+    h = p.ctx().h
+    for b in (u, PacketBatch(m.data, m.data_len, m.offset[40:].copy(), m.caplen[40:].copy())):
+        want = p.DecodeBatch(b, ext=False)
+        arrs = [b.data, b.offset, b.caplen]
+        for a in arrs:
+            check(lib.gpd_host_register(h, a.ctypes.data, a.nbytes), "register")
+        try:
+            assert_same(p.DecodeBatchHost(b, ext=False), want, b, ext=False)
+        finally:
+            for a in arrs:
+                lib.gpd_host_unregister(h, a.ctypes.data)
+
+
 def test_decode_layers_single_packet_api():
     from gopacket_amd import parser as P
     c = [c for c in CASES if c["name"] == "simple_tcp_dlp4"][0]
