@@ -341,7 +341,10 @@ int  gpd_ctx_destroy(gpd_ctx *ctx);
 /* Asynchronous on `stream` (a hipStream_t; NULL = the null stream).  Device pointers. */
 int  gpd_decode(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, void *stream);
 /* Host-memory batch: pinned staging, chunked double-buffered H2D -> decode -> D2H.
- * Synchronous; all pointers in `in`/`out` are host pointers. */
+ * Synchronous; all pointers in `in`/`out` are host pointers.  Arrays registered with
+ * gpd_host_register move by DMA without a staging copy: the packet bytes of a back-to-back
+ * span, its offset and caplen arrays (then without any host pass over the descriptors), and
+ * the result arrays. */
 int  gpd_decode_host(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out);
 int  gpd_sync(gpd_ctx *ctx, void *stream);
 /* Time of the last gpd_decode kernel(s) on `stream`, measured with HIP events recorded on

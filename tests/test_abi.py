@@ -132,3 +132,13 @@ def test_integration_build_command_names_every_source():
     cmd = re.search(r"```sh\nhipcc .*?```", text, re.S).group(0)
     for src in SOURCES:
         assert os.path.relpath(src, ROOT) in cmd, src
+
+
+def test_probe_library_exports_its_entry_points():
+    """bench.py's `roofline.attainable` comes from libgpd_probe.so (a diagnostic beside the
+    product library, not part of include/): it builds for gfx950 and exports both probes."""
+    import ctypes as C
+    from gopacket_amd import build
+    lib = C.CDLL(build.build_probe())
+    for sym in ("gpd_probe_stream", "gpd_probe_stream_ex"):
+        assert hasattr(lib, sym), sym
