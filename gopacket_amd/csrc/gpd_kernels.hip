@@ -2106,7 +2106,11 @@ static hipError_t launch_rs(KParams &P, hipStream_t stream, int num_cus) {
   const size_t lds = ((P.image_words * 4u + 15u) & ~15u) + 4 * (size_t)rs_wave_lds_bytes(STAGE) + 64;
   const uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>((160u * 1024u) / lds, MINW));
   uint64_t blocks = (ntiles + 3) / 4;
-  const uint64_t cap = (uint64_t)num_cus * per_cu * kGridRounds;  // rounds of resident workgroups
+  // rounds of resident workgroups: the AL kernel (VXLAN-sized frames) runs one — each wave's
+  // tiles four times longer — measured 2.2 % faster than four (and 1.6 % than two) on config
+  // 4; config 2, IMIX, pcap64 and the traffic mix keep four (one: +1-2 %, two: within noise;
+  // tools/ab_rounds.sh, profiles/r03/rounds_ab/)
+  const uint64_t cap = (uint64_t)num_cus * per_cu * (AL ? 1u : kGridRounds);
   if (blocks > cap) blocks = cap;
   P.fb_waves = (uint32_t)blocks * 4u;
   if (blocks == 0) return hipSuccess;
