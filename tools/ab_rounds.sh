@@ -1,6 +1,6 @@
 set -e
 mkdir -p gpurun_out/ab
-for c in vxlan imix mixed; do
+for c in ${CONFIGS:-vxlan imix mixed}; do
   for k in 1 2 3; do
     for d in . ab_e4096 ab_e16384; do
       tag=${c}_$(basename $d)_$k
