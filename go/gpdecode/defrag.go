@@ -87,8 +87,23 @@ func (f *Fragment) Err() error {
 //	    whole, _ := defragger.DefragIPv4WithTimestamp(ip4, ts[f.Packet])
 //	}
 //
-// Every other packet skips the defragmenter.
+// Every other packet skips the defragmenter.  A caller that already holds the batch's Result
+// (DecodeBatch, DecodeCapture) uses FragmentsFrom instead: no second decode.
 func (p *BatchDecodingLayerParser) Fragments(b *PacketBatch) ([]Fragment, error) {
+	return p.fragments(b, nil)
+}
+
+// FragmentsFrom is Fragments over the results of a decode already run on b with this parser
+// (r from DecodeBatch, or DecodeCapture of the same packets): the batch and r's status,
+// layers and header-offset words go to the device, and only the hand-off runs there.
+func (p *BatchDecodingLayerParser) FragmentsFrom(b *PacketBatch, r *Result) ([]Fragment, error) {
+	if r == nil || len(r.Status) < len(b.Offset) || len(r.Layers) < len(b.Offset) || len(r.HdrOff) < len(b.Offset) {
+		return nil, errors.New("gpdecode: FragmentsFrom needs the batch's Result (status, layers, header offsets)")
+	}
+	return p.fragments(b, r)
+}
+
+func (p *BatchDecodingLayerParser) fragments(b *PacketBatch, r *Result) ([]Fragment, error) {
 	n := len(b.Offset)
 	if n == 0 {
 		return nil, nil
@@ -106,21 +121,30 @@ func (p *BatchDecodingLayerParser) Fragments(b *PacketBatch) ([]Fragment, error)
 		bufs[k] = d
 		defer d.free()
 	}
-	if err := toDev(bufs[0], unsafe.Pointer(&b.Data[0]), len(b.Data)); err != nil {
-		return nil, err
+	type upload struct {
+		d devBuf
+		p unsafe.Pointer
+		n int
 	}
-	if err := toDev(bufs[1], unsafe.Pointer(&b.Offset[0]), 4*n); err != nil {
-		return nil, err
+	up := []upload{{bufs[0], unsafe.Pointer(&b.Data[0]), len(b.Data)}, {bufs[1], unsafe.Pointer(&b.Offset[0]), 4 * n},
+		{bufs[2], unsafe.Pointer(&b.CapLen[0]), 4 * n}}
+	if r != nil { // the decode's words, as gpd_ip4_fragments reads them
+		up = append(up, upload{bufs[3], unsafe.Pointer(&r.Status[0]), 4 * n},
+			upload{bufs[4], unsafe.Pointer(&r.Layers[0]), 8 * n}, upload{bufs[5], unsafe.Pointer(&r.HdrOff[0]), 4 * n})
 	}
-	if err := toDev(bufs[2], unsafe.Pointer(&b.CapLen[0]), 4*n); err != nil {
-		return nil, err
+	for _, u := range up {
+		if err := toDev(u.d, u.p, u.n); err != nil {
+			return nil, err
+		}
 	}
 	in := C.gpd_batch{data: (*C.uint8_t)(bufs[0].p), data_len: C.uint64_t(len(b.Data)),
 		offset: (*C.uint32_t)(bufs[1].p), caplen: (*C.uint32_t)(bufs[2].p), n: C.uint64_t(n)}
 	res := C.gpd_result{status: (*C.uint32_t)(bufs[3].p), layers: (*C.uint64_t)(bufs[4].p),
 		hdr_off: (*C.uint32_t)(bufs[5].p)}
-	if rc := C.gpd_decode(p.ctx, &in, &res, nil); rc != C.GPD_OK {
-		return nil, lastError("gpd_decode", rc)
+	if r == nil {
+		if rc := C.gpd_decode(p.ctx, &in, &res, nil); rc != C.GPD_OK {
+			return nil, lastError("gpd_decode", rc)
+		}
 	}
 	var cnt C.uint64_t
 	if rc := C.gpd_ip4_fragments(p.ctx, &in, &res, (*C.gpd_ip4_frag)(bufs[6].p), C.uint64_t(n), &cnt, nil); rc != C.GPD_OK {
@@ -144,5 +168,6 @@ func (p *BatchDecodingLayerParser) Fragments(b *PacketBatch) ([]Fragment, error)
 			Verdict: uint8(c.verdict)}
 	}
 	runtime.KeepAlive(b)
+	runtime.KeepAlive(r)
 	return out, nil
 }

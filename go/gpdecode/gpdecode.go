@@ -191,6 +191,15 @@ func (b *PacketBatch) Append(pkt []byte) {
 	b.Data = append(b.Data, pkt...)
 }
 
+// Detail is gpd.h's gpd_detail (same 24-byte layout): the decoded list past the core word's
+// 12 layers and the error's format arguments.  The kernel writes it only for packets with a
+// decode error or more than 12 layers — exactly the packets its fast path leaves to the
+// generic decoder, so asking for it never slows a batch down.
+type Detail struct {
+	Codes      [2]uint64 // decoded[0..31] as 4-bit codes, decoded[k] at bit 4*(k%16) of word k/16
+	Arg0, Arg1 uint32    // the error text's arguments (enum gpd_err in gpd.h)
+}
+
 // Result is the per-packet SoA the kernel writes (include/gpd.h).
 type Result struct {
 	Status   []uint32
@@ -199,13 +208,13 @@ type Result struct {
 	TpHash   []uint64
 	Checksum []uint32
 	HdrOff   []uint32 // gpd.h header offsets word: where the flows' layers sit
+	Detail   []Detail // gpd.h gpd_detail: valid where hasDetail(i)
 }
 
 // DecodeBatch decodes every packet of b (host memory, pinned H2D -> kernel -> D2H).
 func (p *BatchDecodingLayerParser) DecodeBatch(b *PacketBatch) (*Result, error) {
 	n := len(b.Offset)
-	r := &Result{make([]uint32, n), make([]uint64, n), make([]uint64, n), make([]uint64, n), make([]uint32, n),
-		make([]uint32, n)}
+	r := newResult(n)
 	if n == 0 {
 		return r, nil
 	}
@@ -297,42 +306,132 @@ var codeLayerType = [16]gopacket.LayerType{0, layers.LayerTypeEthernet, layers.L
 	layers.LayerTypeTCP, layers.LayerTypeUDP, layers.LayerTypeVXLAN,
 	gopacket.LayerTypePayload, gopacket.LayerTypeFragment, layers.LayerTypeICMPv4, layers.LayerTypeLLC}
 
-// Decoded fills decoded exactly as DecodeLayers would (parser.go:302-316).
-func (r *Result) Decoded(i int, decoded *[]gopacket.LayerType) {
-	*decoded = (*decoded)[:0]
-	n := int(r.Status[i]>>4) & 31
-	for k := 0; k < n && k < C.GPD_CORE_MAX_LAYERS; k++ {
-		*decoded = append(*decoded, codeLayerType[(r.Layers[i]>>(16+4*uint(k)))&15])
+// hasDetail: the kernel wrote Detail[i] (a decode error, or more layers than the core word holds).
+func (r *Result) hasDetail(i int) bool {
+	s := r.Status[i]
+	return s&3 == C.GPD_ST_DECODE_ERROR || (s>>4)&31 > C.GPD_CORE_MAX_LAYERS || s&8 != 0
+}
+
+// ErrStackTooDeep: len(decoded) of the packet exceeds what the result holds (more than 31
+// layers: the status word saturates, and the detail record keeps the first 32).
+var ErrStackTooDeep = errors.New("gpdecode: more than 31 layers decoded; the result keeps the first 32")
+
+// nLayers is len(decoded) (31 when saturated) and code(i, k) the 4-bit code of decoded[k]:
+// from the core word for the first 12, from the detail record past them.
+func (r *Result) nLayers(i int) int { return int(r.Status[i]>>4) & 31 }
+
+func (r *Result) code(i, k int) (uint64, bool) {
+	if k < C.GPD_CORE_MAX_LAYERS {
+		return (r.Layers[i] >> (16 + 4*uint(k))) & 15, true
 	}
+	if k >= 32 || len(r.Detail) <= i || !r.hasDetail(i) {
+		return 0, false
+	}
+	return (r.Detail[i].Codes[k/16] >> (4 * uint(k%16))) & 15, true
+}
+
+// Decoded fills decoded exactly as DecodeLayers would (parser.go:302-316), any depth up to
+// 31 layers (ErrStackTooDeep past that: the status word saturates).
+func (r *Result) Decoded(i int, decoded *[]gopacket.LayerType) error {
+	*decoded = (*decoded)[:0]
+	n := r.nLayers(i)
+	for k := 0; k < n; k++ {
+		c, ok := r.code(i, k)
+		if !ok {
+			return fmt.Errorf("gpdecode: packet %d decoded %d layers; decode with a Detail array", i, n)
+		}
+		*decoded = append(*decoded, codeLayerType[c])
+	}
+	if r.Status[i]&8 != 0 {
+		return ErrStackTooDeep
+	}
+	return nil
 }
 
 // Truncated is parser.Truncated after DecodeLayers on packet i.
 func (r *Result) Truncated(i int) bool { return r.Status[i]&4 != 0 }
 
-// Err is DecodeLayers' return value for packet i. Decode errors carry the
-// reference's text when the format has no arguments; the ext record
-// (gpd_ext_rec.err_arg0/1) supplies the arguments otherwise.
+// Err is DecodeLayers' return value for packet i (parser.go:302-316): nil,
+// gopacket.UnsupportedLayerType, or the failing layer's error with the reference's exact
+// text — its format arguments come from the detail record.
 func (r *Result) Err(i int) error {
 	switch r.Status[i] & 3 {
 	case C.GPD_ST_UNSUPPORTED:
 		return gopacket.UnsupportedLayerType(gopacket.LayerType(r.Layers[i] & 0xFFFF))
 	case C.GPD_ST_DECODE_ERROR:
-		return errors.New(errorText[(r.Status[i]>>9)&63])
+		var a0, a1 uint32
+		if len(r.Detail) > i {
+			a0, a1 = r.Detail[i].Arg0, r.Detail[i].Arg1
+		}
+		return decodeError((r.Status[i]>>9)&63, a0, a1)
 	}
 	return nil
 }
 
-// lastCode is the position-independent kind of the last decoded layer with one of the two
-// codes (the core record holds the first 12 layers).
+// lastCode is the kind of the last decoded layer with one of the two codes, over the whole
+// decoded list (the detail record holds the layers past the core word's 12).
 func (r *Result) lastCode(i int, a, b uint64) uint64 {
-	n := int(r.Status[i]>>4) & 31
+	n := r.nLayers(i)
 	var last uint64
-	for k := 0; k < n && k < C.GPD_CORE_MAX_LAYERS; k++ {
-		if c := (r.Layers[i] >> (16 + 4*uint(k))) & 15; c == a || c == b {
+	for k := 0; k < n; k++ {
+		c, ok := r.code(i, k)
+		if !ok {
+			break
+		}
+		if c == a || c == b {
 			last = c
 		}
 	}
 	return last
+}
+
+// Fill leaves the DecodingLayer objects exactly as DecodeLayers(packet i) leaves the parser's:
+// it repeats the reference's loop (layers_decoder.go:60-79) over the decoded list the kernel
+// reported — each layer's object (the one whose CanDecode holds its type) gets DecodeFromBytes
+// over the previous layer's LayerPayload(), so a kind decoded twice (VXLAN's inner Ethernet and
+// IPv4) ends holding the inner header — and, when the packet's decode failed, hands the failing
+// layer's object its bytes as well (its DecodeFromBytes assigns fields before it returns the
+// error, ip4.go:195-225, tcp.go:234-268, udp.go:35-53).  Pass the same objects the parser was
+// built from.  Returns DecodeLayers' error value for the packet.
+//
+//	res, _ := p.DecodeBatch(&b)
+//	var eth layers.Ethernet; var ip4 layers.IPv4; var tcp layers.TCP; var pl gopacket.Payload
+//	for i := range b.Offset {
+//	    err := p.Fill(res, &b, i, &eth, &ip4, &tcp, &pl)
+//	    ... eth.SrcMAC, ip4.TTL, tcp.Options ...
+//	}
+func (p *BatchDecodingLayerParser) Fill(r *Result, b *PacketBatch, i int, decoders ...gopacket.DecodingLayer) error {
+	var decoded []gopacket.LayerType
+	if err := r.Decoded(i, &decoded); err != nil {
+		return err
+	}
+	find := func(t gopacket.LayerType) gopacket.DecodingLayer {
+		for _, d := range decoders {
+			if d.CanDecode().Contains(t) {
+				return d
+			}
+		}
+		return nil
+	}
+	data := b.Data[b.Offset[i] : b.Offset[i]+b.CapLen[i]]
+	next := p.first
+	for k, t := range decoded {
+		d := find(t)
+		if d == nil {
+			return fmt.Errorf("gpdecode: Fill: no object decodes %v (decoded[%d])", t, k)
+		}
+		if err := d.DecodeFromBytes(data, gopacket.NilDecodeFeedback); err != nil {
+			return fmt.Errorf("gpdecode: Fill: %v failed on the host: %v", t, err)
+		}
+		data, next = d.LayerPayload(), d.NextLayerType()
+	}
+	derr := r.Err(i)
+	if r.Status[i]&3 == C.GPD_ST_DECODE_ERROR && (len(decoded) == 0 || len(data) != 0) {
+		if d := find(next); d != nil {
+			_ = d.DecodeFromBytes(data, gopacket.NilDecodeFeedback) // returns derr again
+		}
+	}
+	return derr
 }
 
 // NetworkFlow is ip4/ip6.NetworkFlow() after DecodeLayers on packet i (ip4.go:63-65,
@@ -380,14 +479,76 @@ func (r *Result) TransportChecksum(i int) (uint16, bool) {
 	return uint16(r.Checksum[i] >> 16), r.Status[i]&(1<<19) != 0
 }
 
-var errorText = map[uint32]string{
-	1: "Ethernet packet too small", 7: "Not all IP header bytes available",
-	14: "IPv6 header option too small", 15: "IPv6 header TLV option too small",
-	16: "Jumbo length TLV data must have length 4", 17: "Jumbo length cannot be less than 65536",
-	18: "IPv6 has jumbo length and IPv6 length is not 0",
-	19: "IPv6 length 0, but HopByHop header does not have jumbogram option",
-	23: "TCP data offset greater than packet length", 29: "vxlan packet too small",
-	30: "ICMP layer less then 8 bytes for ICMPv4 packet", 31: "LLC header too small",
+// decodeError rebuilds the error one reference `return` site (enum gpd_err, file:line in gpd.h)
+// gives, with its format string and its argument types, so err.Error() is the reference's text.
+func decodeError(code, a0, a1 uint32) error {
+	switch code {
+	case 1:
+		return errors.New("Ethernet packet too small") // ethernet.go:42-43
+	case 2:
+		return fmt.Errorf("802.1Q tag length %d too short", int(a0)) // dot1q.go:30-32
+	case 3:
+		return fmt.Errorf("Invalid ip4 header. Length %d less than 20", int(a0)) // ip4.go:189-191
+	case 4:
+		return fmt.Errorf("Invalid (too small) IP length (%d < 20)", uint16(a0)) // ip4.go:220-221
+	case 5:
+		return fmt.Errorf("Invalid (too small) IP header length (%d < 5)", uint8(a0)) // ip4.go:222-223
+	case 6:
+		return fmt.Errorf("Invalid IP header length > IP length (%d > %d)", uint8(a0), uint16(a1)) // :224-225
+	case 7:
+		return errors.New("Not all IP header bytes available") // ip4.go:231-232
+	case 8:
+		return fmt.Errorf("Invalid ip4 option length. Length %d less than 2", int(a0)) // ip4.go:257-259
+	case 9:
+		return fmt.Errorf("IP option length exceeds remaining IP header size, option type %v length %v",
+			uint8(a0), uint8(a1)) // ip4.go:262-264
+	case 10:
+		return fmt.Errorf("Invalid IP option type %v length %d. Must be greater than 2", uint8(a0), uint8(a1)) // :266-267
+	case 11:
+		return fmt.Errorf("Invalid ip6 header. Length %d less than 40", int(a0)) // ip6.go:222-224
+	case 12:
+		return fmt.Errorf("Invalid ip6-extension header. Length %d less than 2", int(a0)) // ip6.go:419-421
+	case 13:
+		return fmt.Errorf("Invalid ip6-extension header. Length %d less than specified length %d",
+			int(a0), int(a1)) // ip6.go:426-427
+	case 14:
+		return errors.New("IPv6 header option too small") // ip6.go:328-330
+	case 15:
+		return errors.New("IPv6 header TLV option too small") // ip6.go:340-342
+	case 16:
+		return errors.New("Jumbo length TLV data must have length 4") // ip6.go:67-68
+	case 17:
+		return fmt.Errorf("Jumbo length cannot be less than %d", 65536) // ip6.go:71-72
+	case 18:
+		return errors.New("IPv6 has jumbo length and IPv6 length is not 0") // ip6.go:257-258
+	case 19:
+		return errors.New("IPv6 length 0, but HopByHop header does not have jumbogram option") // ip6.go:259-260
+	case 20:
+		return fmt.Errorf("IPv6 length 0, but next header is %v, not HopByHop", layers.IPProtocol(a0)) // ip6.go:266-267
+	case 21:
+		return fmt.Errorf("Invalid TCP header. Length %d less than 20", int(a0)) // tcp.go:230-232
+	case 22:
+		return fmt.Errorf("Invalid TCP data offset %d < 5", uint8(a0)) // tcp.go:260-261
+	case 23:
+		return errors.New("TCP data offset greater than packet length") // tcp.go:264-268
+	case 24:
+		return fmt.Errorf("Invalid TCP option length. Length %d less than 2", int(a0)) // tcp.go:286-288
+	case 25:
+		return fmt.Errorf("Invalid TCP option length %d < 2", uint8(a0)) // tcp.go:291-292
+	case 26:
+		return fmt.Errorf("Invalid TCP option length %d exceeds remaining %d bytes", uint8(a0), int(a1)) // tcp.go:293-295
+	case 27:
+		return fmt.Errorf("Invalid UDP header. Length %d less than 8", int(a0)) // udp.go:31-33
+	case 28:
+		return fmt.Errorf("UDP packet too small: %d bytes", uint16(a0)) // udp.go:52-53
+	case 29:
+		return errors.New("vxlan packet too small") // vxlan.go:54-56
+	case 30:
+		return errors.New("ICMP layer less then 8 bytes for ICMPv4 packet") // icmp4.go:221-223
+	case 31:
+		return errors.New("LLC header too small") // llc.go:32-33,42-43
+	}
+	return fmt.Errorf("gpdecode: unknown error code %d", code)
 }
 
 func lastError(what string, rc C.int) error {

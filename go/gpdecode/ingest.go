@@ -351,7 +351,7 @@ func (t *FlowTable) Flows() ([]FlowRecord, error) {
 
 func newResult(n int) *Result {
 	return &Result{make([]uint32, n), make([]uint64, n), make([]uint64, n), make([]uint64, n),
-		make([]uint32, n), make([]uint32, n)}
+		make([]uint32, n), make([]uint32, n), make([]Detail, n)}
 }
 
 // cResult points a gpd_result at r's arrays (r must hold at least one entry per packet).
@@ -366,15 +366,20 @@ func (r *Result) cResult() C.gpd_result {
 		tp_hash:  (*C.uint64_t)(unsafe.Pointer(&r.TpHash[0])),
 		csum:     (*C.uint32_t)(unsafe.Pointer(&r.Checksum[0])),
 		hdr_off:  (*C.uint32_t)(unsafe.Pointer(&r.HdrOff[0])),
+		detail:   (*C.gpd_detail)(unsafe.Pointer(&r.Detail[0])), // same 24-byte layout
 	}
 }
 
 // pin pins r's arrays (the ones cResult points a gpd_result at) until pn.Unpin.
 func (r *Result) pin(pn *runtime.Pinner) {
 	pinFirst(pn, r.Status, r.Layers, r.NetHash, r.TpHash, r.Checksum, r.HdrOff)
+	if len(r.Detail) > 0 {
+		pn.Pin(&r.Detail[0])
+	}
 }
 
 func (r *Result) truncate(n int) {
 	r.Status, r.Layers, r.NetHash = r.Status[:n], r.Layers[:n], r.NetHash[:n]
 	r.TpHash, r.Checksum, r.HdrOff = r.TpHash[:n], r.Checksum[:n], r.HdrOff[:n]
+	r.Detail = r.Detail[:n]
 }

@@ -11,7 +11,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libgpd.so")
 
-GPD_ABI_VERSION = 6
+GPD_ABI_VERSION = 7
 GPD_OK = 0
 GPD_ERR_INVALID = -1
 
@@ -30,7 +30,7 @@ class GpdBatch(C.Structure):
 class GpdResult(C.Structure):
     _fields_ = [("status", C.c_void_p), ("layers", C.c_void_p), ("net_hash", C.c_void_p),
                 ("tp_hash", C.c_void_p), ("csum", C.c_void_p), ("ext", C.c_void_p),
-                ("hdr_off", C.c_void_p), ("records", C.c_void_p)]
+                ("hdr_off", C.c_void_p), ("records", C.c_void_p), ("detail", C.c_void_p)]
 
 
 class GpdTuning(C.Structure):

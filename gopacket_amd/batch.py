@@ -2,8 +2,8 @@
 
 The reference decodes one `[]byte` per call (parser.go:302); a batch holds many
 of them back to back.  Packet starts are 16-byte aligned by default and the
-buffer is padded past its end (include/gpd.h: readable to round_up(len,16)+16),
-so the kernel's 16-byte LDS-DMA never reads outside the allocation.
+buffer is padded past its end (include/gpd.h needs it readable to round_up(len,16);
+PAD adds slack), so the kernel's 16-byte loads never read outside the allocation.
 """
 from __future__ import annotations
 

@@ -195,6 +195,8 @@ int gpd_decode_tpv3(gpd_ctx *ctx, const gpd_tpv3_ring *ring, uint32_t first_bloc
                     uint32_t *blocks_out, int nthreads) {
   if (!ctx || !out || !out->status || !out->layers || !n_out || !blocks_out)
     return gpd::set_error(GPD_ERR_INVALID, "gpd_decode_tpv3: null argument");
+  if (out->ext || out->records)
+    return gpd::set_error(GPD_ERR_INVALID, "gpd_decode_tpv3: SoA results only (no ext records; detail is fine)");
   *n_out = 0;
   *blocks_out = 0;
   std::vector<BlockPlan> plan;
@@ -311,10 +313,13 @@ int gpd_decode_tpv3(gpd_ctx *ctx, const gpd_tpv3_ring *ring, uint32_t first_bloc
   uint64_t *d_ly = static_cast<uint64_t *>(gpd::ctx_scratch(ctx, 6, n * 8));
   uint64_t *d_nh = static_cast<uint64_t *>(gpd::ctx_scratch(ctx, 7, n * 8));
   uint64_t *d_th = static_cast<uint64_t *>(gpd::ctx_scratch(ctx, 8, n * 8));
+  gpd_detail *d_dt = out->detail ? static_cast<gpd_detail *>(gpd::ctx_scratch(ctx, 9, n * sizeof(gpd_detail)))
+                                 : nullptr;
   hipError_t e = hipSuccess;
   for (void *p : {(void *)d_data, (void *)d_off, (void *)d_cap, (void *)d_st, (void *)d_cs,
                   (void *)d_ho, (void *)d_ly, (void *)d_nh, (void *)d_th})
     if (!p) e = hipErrorOutOfMemory;
+  if (out->detail && !d_dt) e = hipErrorOutOfMemory;
   // the walked blocks, ring order from first_block (one copy per contiguous run)
   for (uint64_t j = 0; j < nb && e == hipSuccess;) {
     uint64_t k = j + 1;
@@ -329,7 +334,7 @@ int gpd_decode_tpv3(gpd_ctx *ctx, const gpd_tpv3_ring *ring, uint32_t first_bloc
   if (e == hipSuccess) e = hipMemcpy(d_cap, dcap.data(), n * 4, hipMemcpyHostToDevice);
   if (e == hipSuccess) {
     gpd_batch b{d_data, data_len, d_off, d_cap, n};
-    gpd_result r{d_st, d_ly, d_nh, d_th, d_cs, nullptr, d_ho};
+    gpd_result r{d_st, d_ly, d_nh, d_th, d_cs, nullptr, d_ho, nullptr, d_dt};
     rc = gpd_decode(ctx, &b, &r, nullptr);
     if (rc == GPD_OK) e = hipDeviceSynchronize();
   }
@@ -340,6 +345,8 @@ int gpd_decode_tpv3(gpd_ctx *ctx, const gpd_tpv3_ring *ring, uint32_t first_bloc
     if (e == hipSuccess && out->tp_hash) e = hipMemcpy(out->tp_hash, d_th, n * 8, hipMemcpyDeviceToHost);
     if (e == hipSuccess && out->csum) e = hipMemcpy(out->csum, d_cs, n * 4, hipMemcpyDeviceToHost);
     if (e == hipSuccess && out->hdr_off) e = hipMemcpy(out->hdr_off, d_ho, n * 4, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && out->detail)
+      e = hipMemcpy(out->detail, d_dt, n * sizeof(gpd_detail), hipMemcpyDeviceToHost);
   }
   if (rc) return rc;
   if (e != hipSuccess) return gpd::set_error(GPD_ERR_HIP, "gpd_decode_tpv3: %s", hipGetErrorString(e));

@@ -60,6 +60,7 @@ struct KParams {
   gpd_ext_rec *ext;
   uint32_t *hdr_off;
   gpd_record *rec;             // AoS results (status .. csum NULL)
+  gpd_detail *detail;          // error arguments / deep stacks (generic decoder only; may be NULL)
   const uint32_t *image;       // LUT + ipproto (+ hash tables in HASH mode); staged into LDS
   const uint16_t *pages;       // PAGES mode: two-level page tables in global memory
   uint32_t image_words;

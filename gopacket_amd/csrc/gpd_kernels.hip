@@ -298,10 +298,13 @@ __device__ __forceinline__ uint32_t hdr_word(bool net, uint32_t net_off, bool tp
 
 template <bool EXT, bool PAGES, class S>
 __device__ __forceinline__ Out decode_packet(const S &s, uint32_t caplen, const Tab<PAGES> &T,
-                                             uint32_t first, uint32_t options, gpd_ext_rec *ext) {
+                                             uint32_t first, uint32_t options, gpd_ext_rec *ext,
+                                             gpd_detail *det = nullptr) {
   uint32_t truncated = 0, err = 0, a0 = 0, a1 = 0;
   uint32_t ncount = 0;
-  uint64_t codes = 0, ecodes0 = 0, ecodes1 = 0;
+  // decoded[0..11] in `codes` (the core word), [12..15] in hcodes, [16..31] in ecodes1
+  uint64_t codes = 0, ecodes1 = 0;
+  uint32_t hcodes = 0;
   uint32_t stop = 0, klass = GPD_ST_OK;
   // final state of the objects the fused outputs read: where their addresses / ports were read
   // (ip4_off, ip6_off, tcp_poff, udp_off) and their Contents+Payload (ip4_hl, tcp_off/tcp_tot,
@@ -526,10 +529,8 @@ __device__ __forceinline__ Out decode_packet(const S &s, uint32_t caplen, const 
       {
         const uint64_t code = ent >> 4;
         if (ncount < GPD_CORE_MAX_LAYERS) codes |= code << (16 + 4 * ncount);
-        if (EXT) {
-          if (ncount < 16) ecodes0 |= code << (4 * ncount);
-          else if (ncount < 32) ecodes1 |= code << (4 * (ncount - 16));
-        }
+        else if (ncount < 16) hcodes |= (uint32_t)code << (4 * (ncount - GPD_CORE_MAX_LAYERS));
+        else if (ncount < 32) ecodes1 |= code << (4 * (ncount - 16));
         ncount++;
       }
       obj_valid |= 1u << dec;  // Dec order == enum gpd_obj order
@@ -682,6 +683,16 @@ done:
   o.csum = cs;
   o.hoff = hdr_word(last_net != 0, last_net == 1 ? ip4_off : ip6_off, last_tp != 0,
                     last_tp == 1 ? tcp_poff : udp_off);
+  // decoded[0..15] as the ext / detail records hold them (the core word's 12 codes + hcodes)
+  const uint64_t ecodes0 = (codes >> 16) | ((uint64_t)hcodes << 48);
+  if (det && (klass == GPD_ST_DECODE_ERROR || ncount > GPD_CORE_MAX_LAYERS)) {  // gpd.h gpd_detail
+    gpd_detail d;
+    d.layer_codes[0] = ecodes0;
+    d.layer_codes[1] = ecodes1;
+    d.err_arg0 = klass == GPD_ST_DECODE_ERROR ? a0 : 0;
+    d.err_arg1 = klass == GPD_ST_DECODE_ERROR ? a1 : 0;
+    *det = d;
+  }
   if (EXT) {
     gpd_ext_rec e;
     e.layer_codes[0] = ecodes0;
@@ -1659,14 +1670,16 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void decode_kernel(KParams P) {
     const uint32_t i = td * 64u + lane;
     const uint32_t clen = end_d - off_d;
     if (first_d && big_d)  // larger than a window
-      res = decode_packet<EXT>(GlbSrc{P.data, off_d}, clen, T, P.first, options, EXT ? P.ext + i : nullptr);
+      res = decode_packet<EXT>(GlbSrc{P.data, off_d}, clen, T, P.first, options, EXT ? P.ext + i : nullptr,
+                               P.detail ? P.detail + i : nullptr);
     const uint32_t buf = bufs + cur * STAGE;
     Seg sg{0, 0, 0};
     if (cov_d && (P.options & kDiagSkipDecode)) {  // diagnostics: data movement only
       res = Out{g_lds[buf + ((off_d - Wd.base) & ~15u)], 0, 0, 0, 0, 0};
     } else if (cov_d) {
       const LdsSrc<SWZ> src{buf, off_d - Wd.base};
-      res = decode_packet<EXT>(src, clen, T, P.first, options, EXT ? P.ext + i : nullptr);
+      res = decode_packet<EXT>(src, clen, T, P.first, options, EXT ? P.ext + i : nullptr,
+                               P.detail ? P.detail + i : nullptr);
     }
     PH_MARK(2);  // decode
     if constexpr (COOP) {  // long segments of this window: chunk prefix sums, shared
@@ -2059,7 +2072,9 @@ __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
                        P.tcp_bits, P.udp_bits, P.eth_mult, P.tcp_mult, P.udp_mult};
     constexpr uint32_t K = (uint32_t)STAGE / 64u;
     const uint32_t slot = buf + K * lane;
-    const uint64_t rlim = (((uint64_t)dlen + 15u) & ~15ull) + 16u;  // readable (batch contract)
+    // readable bound of the batch contract (gpd.h gpd_batch: round_up(data_len, 16)): every
+    // 16-byte chunk below it is whole, so no staging load reaches past it
+    const uint64_t rlim = ((uint64_t)dlen + 15u) & ~15ull;
     for (uint32_t j = lane; j - lane < fb_c; j += 64u) {
       const bool live = j < fb_c;
       const uint32_t fi = live ? P.fb_list[fb_start + j] : 0u;
@@ -2075,9 +2090,11 @@ __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
 #pragma unroll
         for (uint32_t k = 0; k < K / 16u; k++) *reinterpret_cast<v4u32 *>(g_lds + slot + 16u * k) = c[k];
         if (live)
-          store_out(P, fi, decode_packet<false>(HybSrc<K>{P.data, off, gb, slot}, len, T, P.first, options, nullptr));
+          store_out(P, fi, decode_packet<false>(HybSrc<K>{P.data, off, gb, slot}, len, T, P.first, options, nullptr,
+                                                P.detail ? P.detail + fi : nullptr));
       } else if (live) {
-        store_out(P, fi, decode_packet<false>(GlbSrc{P.data, off}, len, T, P.first, options, nullptr));
+        store_out(P, fi, decode_packet<false>(GlbSrc{P.data, off}, len, T, P.first, options, nullptr,
+                                              P.detail ? P.detail + fi : nullptr));
       }
     }
   }

@@ -236,6 +236,7 @@ struct gpd_ctx {
     uint64_t *h_th = nullptr, *d_th = nullptr;
     uint32_t *h_hoff = nullptr, *d_hoff = nullptr;
     gpd_ext_rec *h_ext = nullptr, *d_ext = nullptr;
+    gpd_detail *h_det = nullptr, *d_det = nullptr;
     uint32_t *d_pw = nullptr;  // the device pcap walk's per-segment arrays (5 x kPwMaxSeg)
     uint8_t *d_tw = nullptr, *h_tw = nullptr;  // the device TPACKET_V3 walk's tables + results
     hipStream_t stream_out = nullptr;          // its D2H (gpd_decode_tpv3)
@@ -412,11 +413,11 @@ static void free_slots(gpd_ctx *ctx) {
     if (s.stream_out) (void)hipStreamSynchronize(s.stream_out);
     for (void *p : {(void *)s.h_data, (void *)s.h_off, (void *)s.h_len, (void *)s.h_status,
                     (void *)s.h_csum, (void *)s.h_layers, (void *)s.h_nh, (void *)s.h_th,
-                    (void *)s.h_hoff, (void *)s.h_ext, (void *)s.h_tw})
+                    (void *)s.h_hoff, (void *)s.h_ext, (void *)s.h_det, (void *)s.h_tw})
       if (p) (void)hipHostFree(p);
     for (void *p : {(void *)s.d_data, (void *)s.d_off, (void *)s.d_len, (void *)s.d_status,
                     (void *)s.d_csum, (void *)s.d_layers, (void *)s.d_nh, (void *)s.d_th,
-                    (void *)s.d_hoff, (void *)s.d_ext, (void *)s.d_pw, (void *)s.d_tw})
+                    (void *)s.d_hoff, (void *)s.d_ext, (void *)s.d_det, (void *)s.d_pw, (void *)s.d_tw})
       if (p) (void)hipFree(p);
     if (s.stream) (void)hipStreamDestroy(s.stream);
     if (s.stream_out) (void)hipStreamDestroy(s.stream_out);
@@ -516,6 +517,9 @@ float gpd_last_kernel_ms(gpd_ctx *ctx) {
   return ms;
 }
 
+// Largest batch of one call: packet indices and (n + 63) / 64 stay 32-bit (gpd.h gpd_batch).
+constexpr uint64_t kMaxBatchPackets = 0xFFFFFF00ull;
+
 static int check_batch(const gpd_batch *in, const gpd_result *out) {
   if (!in || !out) return set_err(GPD_ERR_INVALID, "gpd_decode: null batch or result");
   if (in->n == 0) return GPD_OK;
@@ -532,6 +536,9 @@ static int check_batch(const gpd_batch *in, const gpd_result *out) {
   if (in->data_len > 0xFFFFFFF0ull)
     return set_err(GPD_ERR_INVALID, "gpd_decode: data_len %llu exceeds the 32-bit offset range",
                    (unsigned long long)in->data_len);
+  if (in->n > kMaxBatchPackets)  // (packet and tile counts stay 32-bit in every kernel)
+    return set_err(GPD_ERR_INVALID, "gpd_decode: batch of %llu packets (max 2^32 - 256)",
+                   (unsigned long long)in->n);
   return GPD_OK;
 }
 
@@ -554,6 +561,7 @@ static int launch(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, hipS
   P.ext = out->ext;
   P.hdr_off = out->hdr_off;
   P.rec = out->records;
+  P.detail = out->detail;
   P.image = ctx->d_image;
   P.pages = ctx->d_pages;
   P.image_words = ctx->image_words;
@@ -628,6 +636,7 @@ static int launch(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, hipS
     Q.csum = out->csum ? out->csum + lo : nullptr;
     Q.ext = out->ext ? out->ext + lo : nullptr;
     Q.hdr_off = out->hdr_off ? out->hdr_off + lo : nullptr;
+    Q.detail = out->detail ? out->detail + lo : nullptr;
     if (gpd::fast_eligible(P)) {  // per-wave counts, two arrays used alternately (a timed
       auto &fb = ctx->fallback[stream];  // launch's counts survive the next launch for the split)
       Q.fb_wcount = fb.wc + (size_t)ctx->num_cus * gpd::kMaxFastWavesPerCU * fb.parity;
@@ -718,9 +727,12 @@ int gpd_ip4_fragments(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *res, 
 }
 
 // ---- host-memory path: chunked, double-buffered pinned H2D -> decode -> D2H ----
-static int alloc_slots(gpd_ctx *ctx, uint64_t bytes, uint64_t pkts, bool ext) {
-  if (ctx->slot_bytes >= bytes && ctx->slot_pkts >= pkts && (!ext || ctx->slot[0].d_ext))
+static int alloc_slots(gpd_ctx *ctx, uint64_t bytes, uint64_t pkts, bool ext, bool det) {
+  if (ctx->slot_bytes >= bytes && ctx->slot_pkts >= pkts && (!ext || ctx->slot[0].d_ext) &&
+      (!det || ctx->slot[0].d_det))
     return GPD_OK;
+  ext = ext || ctx->slot[0].d_ext;  // (a re-allocation keeps what earlier calls asked for)
+  det = det || ctx->slot[0].d_det;
   free_slots(ctx);
   for (auto &s : ctx->slot) {
     HIP_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
@@ -745,6 +757,10 @@ static int alloc_slots(gpd_ctx *ctx, uint64_t bytes, uint64_t pkts, bool ext) {
     if (ext) {
       HIP_TRY(hipHostMalloc(&s.h_ext, pkts * sizeof(gpd_ext_rec), hipHostMallocDefault));
       HIP_TRY(hipMalloc(&s.d_ext, pkts * sizeof(gpd_ext_rec)));
+    }
+    if (det) {
+      HIP_TRY(hipHostMalloc(&s.h_det, pkts * sizeof(gpd_detail), hipHostMallocDefault));
+      HIP_TRY(hipMalloc(&s.d_det, pkts * sizeof(gpd_detail)));
     }
     HIP_TRY(hipMalloc(&s.d_pw, 5ull * gpd::kPwMaxSeg * 4));
   }
@@ -784,6 +800,7 @@ static void drain_slot(gpd_ctx::Slot &s, const gpd_result *out) {
       if (out->tp_hash) std::memcpy(out->tp_hash + s.lo + a, s.h_th + a, c * 8);
       if (out->hdr_off) std::memcpy(out->hdr_off + s.lo + a, s.h_hoff + a, c * 4);
       if (out->ext) std::memcpy(out->ext + s.lo + a, s.h_ext + a, c * sizeof(gpd_ext_rec));
+      if (out->detail) std::memcpy(out->detail + s.lo + a, s.h_det + a, c * sizeof(gpd_detail));
     });
   }
   s.busy = false;
@@ -801,7 +818,8 @@ static hipError_t results_d2h(gpd_ctx *ctx, gpd_ctx::Slot &s, const gpd_result *
              reg(out->csum ? out->csum + lo : nullptr, m * 4) &&
              reg(out->net_hash ? out->net_hash + lo : nullptr, m * 8) &&
              reg(out->tp_hash ? out->tp_hash + lo : nullptr, m * 8) &&
-             reg(out->hdr_off ? out->hdr_off + lo : nullptr, m * 4);
+             reg(out->hdr_off ? out->hdr_off + lo : nullptr, m * 4) &&
+             reg(out->detail ? out->detail + lo : nullptr, m * sizeof(gpd_detail));
   auto cp = [&](void *host, const void *dev, uint64_t bytes) {
     return hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, s.stream);
   };
@@ -815,6 +833,8 @@ static hipError_t results_d2h(gpd_ctx *ctx, gpd_ctx::Slot &s, const gpd_result *
   if (e == hipSuccess && out->hdr_off)
     e = cp(s.direct ? (void *)(out->hdr_off + lo) : (void *)s.h_hoff, s.d_hoff, m * 4);
   if (e == hipSuccess && out->ext) e = cp(s.h_ext, s.d_ext, m * sizeof(gpd_ext_rec));
+  if (e == hipSuccess && out->detail)
+    e = cp(s.direct ? (void *)(out->detail + lo) : (void *)s.h_det, s.d_det, m * sizeof(gpd_detail));
   return e;
 }
 
@@ -823,9 +843,12 @@ int gpd_decode_host(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out) {
   if (!in || !out || !out->status || !out->layers)
     return set_err(GPD_ERR_INVALID, "gpd_decode_host: null batch/result");
   if (in->n == 0) return GPD_OK;
+  if (in->n > kMaxBatchPackets)
+    return set_err(GPD_ERR_INVALID, "gpd_decode_host: batch of %llu packets (max 2^32 - 256)",
+                   (unsigned long long)in->n);
   HIP_TRY(hipSetDevice(ctx->device));
   const uint64_t kPkts = 1u << 20, kBytes = 256ull << 20;
-  int rc = alloc_slots(ctx, kBytes, kPkts, out->ext != nullptr);
+  int rc = alloc_slots(ctx, kBytes, kPkts, out->ext != nullptr, out->detail != nullptr);
   if (rc) return rc;
   SlotGuard guard{ctx};
   uint64_t i = 0;
@@ -862,7 +885,9 @@ int gpd_decode_host(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out) {
     if (span) {
       pos = span_hi - lo16;
       const uint64_t m = j - i;
-      dreg = ctx->is_registered((const uint8_t *)(in->offset + i), m * 4) &&
+      // (the kernel's buffer end lo16 + pos must stay in the 32-bit offset range; past 4 GiB the
+      // offsets are rebased instead)
+      dreg = lo16 + pos <= 0xFFFFFFF0ull && ctx->is_registered((const uint8_t *)(in->offset + i), m * 4) &&
              ctx->is_registered((const uint8_t *)(in->caplen + i), m * 4);
       if (!dreg)
         par_for(m, 1u << 16, [&](uint64_t a, uint64_t b) {
@@ -909,7 +934,7 @@ int gpd_decode_host(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out) {
       b.data_len = lo16 + pos;
     }
     gpd_result r{s.d_status, s.d_layers, s.d_nh, s.d_th, s.d_csum, out->ext ? s.d_ext : nullptr,
-                 out->hdr_off ? s.d_hoff : nullptr};
+                 out->hdr_off ? s.d_hoff : nullptr, nullptr, out->detail ? s.d_det : nullptr};
     rc = launch(ctx, &b, &r, s.stream, false, nullptr, 0, pos);
     if (rc) return rc;
     HIP_TRY(results_d2h(ctx, s, out, i, m));
@@ -997,7 +1022,7 @@ static int decode_pcap_host_walk(gpd_ctx *ctx, const uint8_t *buf, uint64_t len,
   const uint64_t kPkts = 1u << 20, kBytes = 256ull << 20;
   const uint64_t kPart = 1u << 21;  // records per walked part (the first, walked before any
   const uint64_t kPart0 = 1u << 19; // transfer can start, is smaller)
-  int rc = alloc_slots(ctx, kBytes, kPkts, false);
+  int rc = alloc_slots(ctx, kBytes, kPkts, false, out->detail != nullptr);
   if (rc) return rc;
   SlotGuard guard{ctx};
   // The record walk runs one part (kPart records) ahead of the transfers, on a helper thread:
@@ -1087,7 +1112,7 @@ static int decode_pcap_host_walk(gpd_ctx *ctx, const uint8_t *buf, uint64_t len,
       }
       gpd_batch b{s.d_data, span, s.d_off, s.d_len, m};
       gpd_result r{s.d_status, s.d_layers, s.d_nh, s.d_th, s.d_csum, nullptr,
-                   out->hdr_off ? s.d_hoff : nullptr};
+                   out->hdr_off ? s.d_hoff : nullptr, nullptr, out->detail ? s.d_det : nullptr};
       rc = launch(ctx, &b, &r, s.stream, false);
       if (rc) return rc;
       e = results_d2h(ctx, s, out, done + i, m);
@@ -1166,7 +1191,7 @@ static int decode_device_walk(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, co
     mean = std::max<uint64_t>(16, (R.next_pos - pos) / R.n);
   }
   int rc = alloc_slots(ctx, std::max<uint64_t>(ctx->slot_bytes, kChunk + margin + 64),
-                       std::max<uint64_t>(ctx->slot_pkts, cap_pkts), false);
+                       std::max<uint64_t>(ctx->slot_pkts, cap_pkts), false, out->detail != nullptr);
   if (rc) return rc;
   SlotGuard guard{ctx};
   // Chunk k's work on slot k & 1: its bytes H2D, then (after chunk k-1's walk) its walk, its
@@ -1220,7 +1245,8 @@ static int decode_device_walk(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, co
     if (e == hipSuccess) e = gpd::launch_pcap_fill(A, s.stream);
     if (e != hipSuccess) return set_err(GPD_ERR_HIP, "gpd_decode_pcap: device walk: %s", hipGetErrorString(e));
     gpd_batch b{s.d_data, T, s.d_off, s.d_len, cap_pkts};
-    gpd_result r{s.d_status, s.d_layers, s.d_nh, s.d_th, s.d_csum, nullptr, out->hdr_off ? s.d_hoff : nullptr};
+    gpd_result r{s.d_status, s.d_layers, s.d_nh, s.d_th, s.d_csum, nullptr, out->hdr_off ? s.d_hoff : nullptr,
+                 nullptr, out->detail ? s.d_det : nullptr};
     return launch(ctx, &b, &r, s.stream, false, &dc->n, std::max<uint64_t>(1, own / mean));
   };
   uint64_t B = pos & ~15ull;  // chunk base (16-byte aligned: the decoder's batch buffer)
@@ -1320,6 +1346,7 @@ int gpd_decode_pcap_at(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, const gpd
   rest.tp_hash = shift(out->tp_hash);
   rest.csum = shift(out->csum);
   rest.hdr_off = shift(out->hdr_off);
+  rest.detail = shift(out->detail);
   uint64_t k = 0;
   const int rc = decode_pcap_host_walk(ctx, buf, len, info, at, max_n - done, &rest, &k, next_pos, stop, nthreads);
   *n_out = done + k;
@@ -1346,8 +1373,9 @@ constexpr uint64_t kTwTab = kTwMaxBlocks * sizeof(gpd::TwBlock), kTwSt = kTwMaxB
 // A group's per-packet arrays packed into one region, so one D2H brings them back: decode
 // results, caplen (the walk's, the decode's input), then the capture info, each array
 // 256-byte aligned.  The region is laid out for the group's packet count m.
-enum TwArr { kLayers, kNh, kTh, kStatus, kCsum, kHoff, kCap, kCiOff, kCiTs, kCiWire, kCiIfx, kCiVlan, kCiTci, kTwN };
-constexpr uint64_t kTwW[kTwN] = {8, 8, 8, 4, 4, 4, 4, 8, 8, 4, 4, 4, 4};
+enum TwArr { kLayers, kNh, kTh, kStatus, kCsum, kHoff, kDet, kCap, kCiOff, kCiTs, kCiWire, kCiIfx, kCiVlan, kCiTci,
+             kTwN };
+constexpr uint64_t kTwW[kTwN] = {8, 8, 8, 4, 4, 4, sizeof(gpd_detail), 4, 8, 8, 4, 4, 4, 4};
 struct TwLay {
   uint64_t off[kTwN + 1];  // off[kCiOff]: the end of the region without capture info
   explicit TwLay(uint64_t m) {
@@ -1381,7 +1409,7 @@ int gpd::decode_tpv3_device(gpd_ctx *ctx, const gpd_tpv3_ring &R, const std::vec
   if (nthreads <= 0) nthreads = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
   HIP_TRY(hipSetDevice(ctx->device));
   int rc = alloc_slots(ctx, std::max<uint64_t>(ctx->slot_bytes, kTwGroup),
-                       std::max<uint64_t>(ctx->slot_pkts, kTwPkts), false);
+                       std::max<uint64_t>(ctx->slot_pkts, kTwPkts), false, false);
   if (rc) return rc;
   for (auto &s : ctx->slot) {
     if (!s.d_tw) HIP_TRY(hipMalloc(&s.d_tw, tw_dreg() + kTwRegion));
@@ -1403,7 +1431,7 @@ int gpd::decode_tpv3_device(gpd_ctx *ctx, const gpd_tpv3_ring &R, const std::vec
   };
   std::vector<Group> grp;
   // the caller's array for each region array (NULL: not asked for)
-  void *dst[kTwN] = {out->layers, out->net_hash, out->tp_hash, out->status, out->csum, out->hdr_off,
+  void *dst[kTwN] = {out->layers, out->net_hash, out->tp_hash, out->status, out->csum, out->hdr_off, out->detail,
                      ci ? pk->caplen : nullptr, ci ? pk->offset : nullptr, ci ? pk->ts_ns : nullptr,
                      ci ? pk->wire_len : nullptr, ci ? pk->ifindex : nullptr, ci ? pk->vlan : nullptr,
                      ci ? pk->vlan_tci : nullptr};
@@ -1494,7 +1522,8 @@ int gpd::decode_tpv3_device(gpd_ctx *ctx, const gpd_tpv3_ring &R, const std::vec
       gpd_result r{reinterpret_cast<uint32_t *>(dev(kStatus)), reinterpret_cast<uint64_t *>(dev(kLayers)),
                    reinterpret_cast<uint64_t *>(dev(kNh)), reinterpret_cast<uint64_t *>(dev(kTh)),
                    reinterpret_cast<uint32_t *>(dev(kCsum)), nullptr,
-                   out->hdr_off ? reinterpret_cast<uint32_t *>(dev(kHoff)) : nullptr};
+                   out->hdr_off ? reinterpret_cast<uint32_t *>(dev(kHoff)) : nullptr, nullptr,
+                   out->detail ? reinterpret_cast<gpd_detail *>(dev(kDet)) : nullptr};
       if ((rc = launch(ctx, &bt, &r, s.stream, false))) return rc;
     }
     HIP_TRY(hipEventRecord(ctx->ev_twdec[k & 3], s.stream));

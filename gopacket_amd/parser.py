@@ -24,7 +24,7 @@ import numpy as np
 from . import layers as L
 from ._lib import GPD_ERR_PCAP, GpdBatch, GpdConfig, GpdResult, check, lib
 from .batch import PAD, PacketBatch
-from .results import EXT_DTYPE, RECORD_DTYPE, BatchResult
+from .results import DETAIL_DTYPE, EXT_DTYPE, RECORD_DTYPE, BatchResult
 
 DEC_ETHERNET, DEC_DOT1Q, DEC_IPV4, DEC_IPV6, DEC_IPV6_EXT = 1, 2, 4, 8, 16
 DEC_TCP, DEC_UDP, DEC_VXLAN, DEC_PAYLOAD, DEC_FRAGMENT = 32, 64, 128, 256, 512
@@ -160,10 +160,12 @@ class DeviceBatch:
 
 class DeviceResult:
     """Results in HBM — the SoA arrays, or (records=True) one 32-B gpd_record per packet;
-    .to_host() gives a BatchResult either way."""
+    .to_host() gives a BatchResult either way.  detail=True adds the gpd_detail array (the
+    error arguments and deep stacks, written by the generic decoder only: the fast path stays
+    on)."""
 
     def __init__(self, n: int, device: int = 0, ext: bool = False, hdr_off: bool = True,
-                 records: bool = False):
+                 records: bool = False, detail: bool = False):
         torch = _torch()
         dev = torch.device("cuda", device)
         self.n = n
@@ -179,25 +181,25 @@ class DeviceResult:
             self.csum = torch.empty(n, dtype=torch.int32, device=dev)
         self.ext = torch.empty(n * EXT_DTYPE.itemsize, dtype=torch.uint8, device=dev) if ext else None
         self.hdr_off = torch.empty(n, dtype=torch.int32, device=dev) if hdr_off else None
+        self.detail = torch.zeros(n * DETAIL_DTYPE.itemsize, dtype=torch.uint8, device=dev) if detail else None
 
     def c_result(self) -> GpdResult:
         p = lambda t: t.data_ptr() if t is not None else None
         return GpdResult(p(self.status), p(self.layers), p(self.net_hash), p(self.tp_hash),
-                         p(self.csum), p(self.ext), p(self.hdr_off), p(self.records))
+                         p(self.csum), p(self.ext), p(self.hdr_off), p(self.records), p(self.detail))
 
     def to_host(self) -> BatchResult:
         u = lambda t, dt: t.cpu().numpy().view(dt)
+        ext = self.ext.cpu().numpy().view(EXT_DTYPE) if self.ext is not None else None
+        hoff = u(self.hdr_off, np.uint32) if self.hdr_off is not None else None
+        det = self.detail.cpu().numpy().view(DETAIL_DTYPE) if self.detail is not None else None
         if self.records is not None:
             r = self.records.cpu().numpy().view(RECORD_DTYPE)
             return BatchResult(r["status"].copy(), r["layers"].copy(), r["net_hash"].copy(),
-                               r["tp_hash"].copy(), r["csum"].copy(),
-                               self.ext.cpu().numpy().view(EXT_DTYPE) if self.ext is not None else None,
-                               u(self.hdr_off, np.uint32) if self.hdr_off is not None else None)
+                               r["tp_hash"].copy(), r["csum"].copy(), ext, hoff, det)
         return BatchResult(u(self.status, np.uint32), u(self.layers, np.uint64),
                            u(self.net_hash, np.uint64), u(self.tp_hash, np.uint64),
-                           u(self.csum, np.uint32),
-                           self.ext.cpu().numpy().view(EXT_DTYPE) if self.ext is not None else None,
-                           u(self.hdr_off, np.uint32) if self.hdr_off is not None else None)
+                           u(self.csum, np.uint32), ext, hoff, det)
 
 
 class DecodingLayerParser:
@@ -273,35 +275,36 @@ class DecodingLayerParser:
         check(lib.gpd_decode(self.ctx().h, C.byref(b), C.byref(r), C.c_void_p(stream.cuda_stream)),
               "gpd_decode")
 
-    def DecodeBatch(self, batch: PacketBatch, ext: bool = False) -> BatchResult:
-        """Decode every packet of a host batch on the GPU (H2D, kernel, D2H)."""
+    def DecodeBatch(self, batch: PacketBatch, ext: bool = False, detail: bool = True) -> BatchResult:
+        """Decode every packet of a host batch on the GPU (H2D, kernel, D2H).  With detail (the
+        default) res.err(i) carries the reference's exact text and res.decoded(i) any depth,
+        and the batch keeps the fast path; ext adds the layer records (generic path)."""
         torch = _torch()
         db = DeviceBatch(batch, self.device)
-        dr = DeviceResult(batch.n, self.device, ext)
+        dr = DeviceResult(batch.n, self.device, ext, detail=detail)
         self.decode_device(db, dr)
         torch.cuda.synchronize(self.device)
         return dr.to_host()
 
     def DecodeBatchHost(self, batch: PacketBatch, ext: bool = False,
-                        out: Optional[BatchResult] = None) -> BatchResult:
+                        out: Optional[BatchResult] = None, detail: bool = False) -> BatchResult:
         """Host-memory path through gpd_decode_host (pinned, chunked, double-buffered).
-        `out` reuses a result of the same size (no allocation per call)."""
+        `out` reuses a result of the same size (no allocation per call; its detail array, if
+        any, is filled)."""
         n = batch.n
         res = out if out is not None else BatchResult(
             np.zeros(n, np.uint32), np.zeros(n, np.uint64), np.zeros(n, np.uint64),
             np.zeros(n, np.uint64), np.zeros(n, np.uint32), np.zeros(n, EXT_DTYPE) if ext else None,
-            np.zeros(n, np.uint32))
+            np.zeros(n, np.uint32), np.zeros(n, DETAIL_DTYPE) if detail else None)
         b = GpdBatch(batch.data.ctypes.data, batch.data_len, batch.offset.ctypes.data,
                      batch.caplen.ctypes.data, n)
-        r = GpdResult(res.status.ctypes.data, res.layers.ctypes.data, res.net_hash.ctypes.data,
-                      res.tp_hash.ctypes.data, res.csum.ctypes.data,
-                      res.ext.ctypes.data if res.ext is not None else None,
-                      res.hdr_off.ctypes.data if res.hdr_off is not None else None)
+        r = _c_result(res)
         check(lib.gpd_decode_host(self.ctx().h, C.byref(b), C.byref(r)), "gpd_decode_host")
         return res
 
     def DecodePcap(self, cap: np.ndarray, max_n: Optional[int] = None, nthreads: int = 0,
-                   data_len: Optional[int] = None, out: Optional[BatchResult] = None):
+                   data_len: Optional[int] = None, out: Optional[BatchResult] = None,
+                   detail: bool = False):
         """A whole in-memory capture (pcap.capture_array) through gpd_decode_pcap: records
         indexed natively, their raw bytes chunked host -> device, decoded, results back.
         Returns (BatchResult of the decoded records, number of records, error text or None —
@@ -316,9 +319,8 @@ class DecodingLayerParser:
         else:
             res = BatchResult(np.zeros(m, np.uint32), np.zeros(m, np.uint64), np.zeros(m, np.uint64),
                               np.zeros(m, np.uint64), np.zeros(m, np.uint32), None,
-                              np.zeros(m, np.uint32))
-        r = GpdResult(res.status.ctypes.data, res.layers.ctypes.data, res.net_hash.ctypes.data,
-                      res.tp_hash.ctypes.data, res.csum.ctypes.data, None, res.hdr_off.ctypes.data)
+                              np.zeros(m, np.uint32), np.zeros(m, DETAIL_DTYPE) if detail else None)
+        r = _c_result(res)
         n, nxt, stop = C.c_uint64(), C.c_uint64(), C.c_int()
         rc = lib.gpd_decode_pcap(self.ctx().h, cap.ctypes.data, dl, m, C.byref(r), C.byref(n),
                                  C.byref(nxt), C.byref(stop), int(nthreads))
@@ -328,9 +330,7 @@ class DecodingLayerParser:
         elif rc != 0:
             check(rc, "gpd_decode_pcap")
         k = n.value
-        out = BatchResult(res.status[:k], res.layers[:k], res.net_hash[:k], res.tp_hash[:k],
-                          res.csum[:k], None, res.hdr_off[:k])
-        return out, k, err
+        return _head(res, k), k, err
 
     def DecodePcapAt(self, cap: np.ndarray, info, pos: int, max_n: int, out: BatchResult,
                      nthreads: int = 0, data_len: Optional[int] = None):
@@ -341,8 +341,7 @@ class DecodingLayerParser:
         dl = cap.shape[0] - PAD if data_len is None else int(data_len)
         if len(out.status) < max_n or out.hdr_off is None:
             raise ValueError("DecodePcapAt: out must hold max_n entries, with hdr_off")
-        r = GpdResult(out.status.ctypes.data, out.layers.ctypes.data, out.net_hash.ctypes.data,
-                      out.tp_hash.ctypes.data, out.csum.ctypes.data, None, out.hdr_off.ctypes.data)
+        r = _c_result(out)
         n, nxt, stop = C.c_uint64(), C.c_uint64(), C.c_int()
         rc = lib.gpd_decode_pcap_at(self.ctx().h, cap.ctypes.data, dl, C.byref(info), int(pos),
                                     int(max_n), C.byref(r), C.byref(n), C.byref(nxt), C.byref(stop),
@@ -369,8 +368,7 @@ class DecodingLayerParser:
             np.zeros(max_n, np.uint64), np.zeros(max_n, np.uint32), None, np.zeros(max_n, np.uint32))
         if len(res.status) < max_n or res.hdr_off is None or len(ci.offset) < max_n:
             raise ValueError("DecodeTPv3: out / ci must hold max_n entries (out with hdr_off)")
-        r = GpdResult(res.status.ctypes.data, res.layers.ctypes.data, res.net_hash.ctypes.data,
-                      res.tp_hash.ctypes.data, res.csum.ctypes.data, None, res.hdr_off.ctypes.data)
+        r = _c_result(res)
         n, nb = C.c_uint64(), C.c_uint32()
         check(lib.gpd_decode_tpv3(self.ctx().h, C.byref(ring.c), ring.offset % ring.num_blocks,
                                   ring.num_blocks if max_blocks is None else int(max_blocks),
@@ -378,17 +376,28 @@ class DecodingLayerParser:
                                   C.byref(ci.c()), C.byref(n), C.byref(nb), int(nthreads)),
               "gpd_decode_tpv3")
         k = n.value
-        out = BatchResult(res.status[:k], res.layers[:k], res.net_hash[:k], res.tp_hash[:k],
-                          res.csum[:k], None, res.hdr_off[:k])
-        return out, ci.head(k), nb.value
+        return _head(res, k), ci.head(k), nb.value
 
     def DecodeLayers(self, data: bytes, decoded: list):
         """parser.go:302-316 for one packet: fills `decoded`, sets self.Truncated, returns the
         error value (None on success)."""
-        res = self.DecodeBatch(PacketBatch.from_packets([data]), ext=True)
+        res = self.DecodeBatch(PacketBatch.from_packets([data]), detail=True)
         decoded[:] = res.decoded(0)
         self.Truncated = res.truncated(0)
         return res.err(0)
+
+
+def _c_result(res: BatchResult) -> GpdResult:
+    """The C-ABI result struct over a host BatchResult's arrays (SoA; absent arrays NULL)."""
+    p = lambda a: a.ctypes.data if a is not None else None
+    return GpdResult(p(res.status), p(res.layers), p(res.net_hash), p(res.tp_hash), p(res.csum),
+                     p(res.ext), p(res.hdr_off), None, p(res.detail))
+
+
+def _head(res: BatchResult, k: int) -> BatchResult:
+    h = lambda a: a[:k] if a is not None else None
+    return BatchResult(h(res.status), h(res.layers), h(res.net_hash), h(res.tp_hash), h(res.csum),
+                       h(res.ext), h(res.hdr_off), h(res.detail))
 
 
 def NewDecodingLayerParser(first: int, *decoders, device: int = 0) -> DecodingLayerParser:

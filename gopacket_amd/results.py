@@ -30,6 +30,10 @@ EXT_DTYPE = np.dtype([("layer_codes", "<u8", (2,)), ("err_arg0", "<u4"), ("err_a
                       ("obj_valid", "<u2"), ("err_obj", "u1"), ("err_wrote", "u1"), ("err_off", "<u4"),
                       ("obj", LAYER_REC_DTYPE, (12,))])
 assert EXT_DTYPE.itemsize == 224
+# gpd_detail (gpd.h): the first 24 bytes of the ext record, written for decode errors and
+# stacks deeper than the core word's 12 layers only
+DETAIL_DTYPE = np.dtype([("layer_codes", "<u8", (2,)), ("err_arg0", "<u4"), ("err_arg1", "<u4")])
+assert DETAIL_DTYPE.itemsize == 24
 
 ST_OK, ST_UNSUPPORTED, ST_DECODE_ERROR = 0, 1, 2
 
@@ -59,22 +63,33 @@ class BatchResult:
     csum: Optional[np.ndarray] = None
     ext: Optional[np.ndarray] = None  # EXT_DTYPE[n]
     hdr_off: Optional[np.ndarray] = None  # uint32[n], gpd.h header offsets word
+    detail: Optional[np.ndarray] = None  # DETAIL_DTYPE[n]: valid where has_detail(i)
 
     def __len__(self):
         return int(self.status.shape[0])
 
     # --- the DecodeLayers outputs -------------------------------------------------
+    def has_detail(self, i: int) -> bool:
+        """Whether the kernel wrote packet i's detail record (gpd.h gpd_detail): a decode
+        error, or more layers than the core word holds."""
+        s = int(self.status[i])
+        return st_class(s) == ST_DECODE_ERROR or st_nlayers(s) > 12 or bool((s >> 3) & 1)
+
     def decoded(self, i: int) -> list:
         """The `decoded` slice (LayerType values), layers_decoder.go:69."""
         s = int(self.status[i])
         n = st_nlayers(s)
+        words = None
         if self.ext is not None:
             words = self.ext["layer_codes"][i]
+        elif n > 12 and self.detail is not None:
+            words = self.detail["layer_codes"][i]
+        if words is not None:
             n = min(n, 32)
             return [CODE_TO_LAYERTYPE[(int(words[k // 16]) >> (4 * (k % 16))) & 15] for k in range(n)]
         w = int(self.layers[i])
         if n > 12:
-            raise ValueError(f"packet {i}: {n} layers exceed the core record; decode with ext=True")
+            raise ValueError(f"packet {i}: {n} layers exceed the core record; decode with detail or ext")
         return [CODE_TO_LAYERTYPE[(w >> (16 + 4 * k)) & 15] for k in range(n)]
 
     def stop_type(self, i: int) -> int:
@@ -92,6 +107,8 @@ class BatchResult:
         a0 = a1 = 0
         if self.ext is not None:
             a0, a1 = int(self.ext["err_arg0"][i]), int(self.ext["err_arg1"][i])
+        elif self.detail is not None:
+            a0, a1 = int(self.detail["err_arg0"][i]), int(self.detail["err_arg1"][i])
         return DecodeError(st_errcode(s), a0, a1)
 
     def truncated(self, i: int) -> bool:
@@ -135,7 +152,8 @@ class BatchResult:
         return (c0, c0 + int(r["contents_len"])), (p0, p0 + int(r["payload_len"]))
 
 
-def empty_result(n: int, ext: bool = False) -> BatchResult:
+def empty_result(n: int, ext: bool = False, detail: bool = False) -> BatchResult:
     return BatchResult(np.zeros(n, np.uint32), np.zeros(n, np.uint64), np.zeros(n, np.uint64),
                        np.zeros(n, np.uint64), np.zeros(n, np.uint32),
-                       np.zeros(n, EXT_DTYPE) if ext else None, np.zeros(n, np.uint32))
+                       np.zeros(n, EXT_DTYPE) if ext else None, np.zeros(n, np.uint32),
+                       np.zeros(n, DETAIL_DTYPE) if detail else None)

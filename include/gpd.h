@@ -46,10 +46,11 @@
 extern "C" {
 #endif
 
-#define GPD_ABI_VERSION 6  /* 2: ICMPv4 + LLC, 12 objects, 224-B ext; 3: gpd_result.hdr_off;
+#define GPD_ABI_VERSION 7  /* 2: ICMPv4 + LLC, 12 objects, 224-B ext; 3: gpd_result.hdr_off;
                               4: gpd_ctx_set_tuning; 5: gpd_tuning.header_once,
                               gpd_tuning.device_walk, gpd_result.records; 6: outputs follow the
-                              objects as a failing call leaves them; ext err_obj/err_wrote/err_off */
+                              objects as a failing call leaves them; ext err_obj/err_wrote/err_off;
+                              7: gpd_result.detail (error arguments and deep stacks without ext) */
 
 /* ---- gopacket LayerType numbers (layertypes.go:14-154, decode.go:105-116) ---- */
 #define GPD_LT_ZERO            0
@@ -253,6 +254,21 @@ typedef struct gpd_ext_rec {
   gpd_layer_rec obj[GPD_NOBJ];
 } gpd_ext_rec;
 
+/* Optional per-packet detail record (24 B; the first 24 bytes of gpd_ext_rec, same meaning):
+ * what a caller needs beyond the core words to rebuild DecodeLayers' exact return values —
+ * the format arguments of the decode error (parser.go:302-316 returns the layer's error, e.g.
+ * ip4.go:220-225, tcp.go:260-295, udp.go:31-53) and the decoded list past the core record's
+ * 12 layers.  It is written ONLY for packets whose status has class GPD_ST_DECODE_ERROR or
+ * n_layers > GPD_CORE_MAX_LAYERS (saturated included); the entries of every other packet are
+ * left unspecified (gpd_decode leaves them untouched).  Those packets are exactly the ones the
+ * fast kernel hands to the generic decoder, so asking for detail costs the fast path nothing:
+ * it never forces the generic path for the batch, as ext does.                               */
+typedef struct gpd_detail {
+  uint64_t layer_codes[2];  /* decoded[0..31] as 4-bit codes, decoded[i] at bit 4*(i%16) of word i/16 */
+  uint32_t err_arg0;        /* first %d/%v argument of the error text (enum gpd_err), else 0 */
+  uint32_t err_arg1;        /* second argument, if any, else 0 */
+} gpd_detail;
+
 /* ---- context configuration ---- */
 typedef struct gpd_config {
   uint32_t first_layer;      /* LayerType the parser starts with (NewDecodingLayerParser first) */
@@ -310,7 +326,9 @@ typedef struct gpd_record {
  * NULL and each packet's five words are written as one 32-byte gpd_record instead (one
  * stream of 2 x 16-byte stores per packet rather than five arrays); ext and hdr_off stay
  * separate arrays.  The host-memory entry points (gpd_decode_host, gpd_decode_pcap*,
- * TPACKET_V3) take the SoA form only. */
+ * TPACKET_V3) take the SoA form only.
+ * detail (every entry point): see gpd_detail — written for decode errors and > 12-layer stacks
+ * only.  ext (gpd_decode, gpd_decode_host) forces the generic decoder for the whole batch. */
 typedef struct gpd_result {
   uint32_t    *status;
   uint64_t    *layers;
@@ -320,6 +338,7 @@ typedef struct gpd_result {
   gpd_ext_rec *ext;
   uint32_t    *hdr_off;    /* header offsets word (above) */
   gpd_record  *records;    /* AoS form of the first five (see above) */
+  gpd_detail  *detail;     /* error arguments / deep stacks (ABI 7) */
 } gpd_result;
 
 typedef struct gpd_ctx gpd_ctx;

@@ -3,7 +3,7 @@
  * go/gpdecode does), with no Python or PyTorch in the process, so libgpd.so runs on
  * /opt/rocm's HIP runtime exactly as it would under Go.
  *
- *   abi_host BATCH_FILE
+ *   abi_host BATCH_FILE [ERR_OUT PROTO_NAMES]
  *
  * BATCH_FILE: u64 data_len, u64 n, u32 decoders, u32 options, data[data_len], u32 offset[n],
  * u32 caplen[n].  The batch is decoded three ways and every output word is compared:
@@ -20,6 +20,12 @@
  * packets whose last network layer is an IPv4 header with MoreFragments or an offset and no
  * DF, in packet order, with the key and fields of those header bytes and the securityChecks
  * verdict (ip4defrag/defrag.go:162-198) recomputed here.
+ * Every path also fills the gpd_detail array (gpd.h): for each packet with a decode error or
+ * more than 12 layers it must equal the oracle's ext prefix (decoded list, error arguments) in
+ * all three paths.  With ERR_OUT, the error value DecodeLayers returns (parser.go:302-326) is
+ * rebuilt from the device's status + detail words alone — the reference's format strings, with
+ * IPProtocol.String() names read from PROTO_NAMES (256 lines) — and written as "i<TAB>text"
+ * lines, one per failing packet, for the Python test to compare with the oracle's texts.
  * Prints "abi_host ok N F R" (F = flows, R = fragments) and exits 0 when everything agrees.
  */
 #include <stddef.h>
@@ -57,6 +63,7 @@
 typedef struct {
   uint32_t *status, *csum, *hdr_off;
   uint64_t *layers, *net_hash, *tp_hash;
+  gpd_detail *detail;
 } res_t;
 
 static res_t res_alloc(uint64_t n) {
@@ -67,7 +74,71 @@ static res_t res_alloc(uint64_t n) {
   r.layers = calloc(n, 8);
   r.net_hash = calloc(n, 8);
   r.tp_hash = calloc(n, 8);
+  r.detail = calloc(n + 1, sizeof(gpd_detail));
   return r;
+}
+
+/* gpd.h gpd_detail: written for decode errors and stacks deeper than the core word */
+static int has_detail(uint32_t st) {
+  return GPD_STATUS_CLASS(st) == GPD_ST_DECODE_ERROR || GPD_STATUS_NLAYERS(st) > GPD_CORE_MAX_LAYERS ||
+         GPD_STATUS_SATURATED(st);
+}
+
+/* the detail records of `a` vs the oracle's ext records (their first 24 bytes: same layout) */
+static int detail_cmp(const char *what, const res_t *a, const gpd_ext_rec *ext, uint64_t n) {
+  for (uint64_t i = 0; i < n; i++) {
+    if (!has_detail(a->status[i])) continue;
+    const gpd_detail *d = &a->detail[i];
+    if (d->layer_codes[0] != ext[i].layer_codes[0] || d->layer_codes[1] != ext[i].layer_codes[1] ||
+        d->err_arg0 != ext[i].err_arg0 || d->err_arg1 != ext[i].err_arg1) {
+      fprintf(stderr, "%s: packet %llu detail differs: codes %016llx %016llx/%016llx %016llx args %u %u/%u %u\n",
+              what, (unsigned long long)i, (unsigned long long)d->layer_codes[0],
+              (unsigned long long)d->layer_codes[1], (unsigned long long)ext[i].layer_codes[0],
+              (unsigned long long)ext[i].layer_codes[1], d->err_arg0, d->err_arg1, ext[i].err_arg0,
+              ext[i].err_arg1);
+      return 1;
+    }
+  }
+  return 0;
+}
+
+/* The error text of enum gpd_err `code` with the detail record's arguments: the format string
+ * at each `return ...error` site of the reference (the file:line list is in gpd.h). */
+static void error_text(char *out, size_t cap, uint32_t code, uint32_t a0, uint32_t a1, char names[256][64]) {
+  switch (code) {
+    case 1: snprintf(out, cap, "Ethernet packet too small"); break;
+    case 2: snprintf(out, cap, "802.1Q tag length %u too short", a0); break;
+    case 3: snprintf(out, cap, "Invalid ip4 header. Length %u less than 20", a0); break;
+    case 4: snprintf(out, cap, "Invalid (too small) IP length (%u < 20)", a0); break;
+    case 5: snprintf(out, cap, "Invalid (too small) IP header length (%u < 5)", a0); break;
+    case 6: snprintf(out, cap, "Invalid IP header length > IP length (%u > %u)", a0, a1); break;
+    case 7: snprintf(out, cap, "Not all IP header bytes available"); break;
+    case 8: snprintf(out, cap, "Invalid ip4 option length. Length %u less than 2", a0); break;
+    case 9: snprintf(out, cap, "IP option length exceeds remaining IP header size, option type %u length %u", a0, a1); break;
+    case 10: snprintf(out, cap, "Invalid IP option type %u length %u. Must be greater than 2", a0, a1); break;
+    case 11: snprintf(out, cap, "Invalid ip6 header. Length %u less than 40", a0); break;
+    case 12: snprintf(out, cap, "Invalid ip6-extension header. Length %u less than 2", a0); break;
+    case 13: snprintf(out, cap, "Invalid ip6-extension header. Length %u less than specified length %u", a0, a1); break;
+    case 14: snprintf(out, cap, "IPv6 header option too small"); break;
+    case 15: snprintf(out, cap, "IPv6 header TLV option too small"); break;
+    case 16: snprintf(out, cap, "Jumbo length TLV data must have length 4"); break;
+    case 17: snprintf(out, cap, "Jumbo length cannot be less than 65536"); break;
+    case 18: snprintf(out, cap, "IPv6 has jumbo length and IPv6 length is not 0"); break;
+    case 19: snprintf(out, cap, "IPv6 length 0, but HopByHop header does not have jumbogram option"); break;
+    case 20: snprintf(out, cap, "IPv6 length 0, but next header is %s, not HopByHop", names[a0 & 255]); break;
+    case 21: snprintf(out, cap, "Invalid TCP header. Length %u less than 20", a0); break;
+    case 22: snprintf(out, cap, "Invalid TCP data offset %u < 5", a0); break;
+    case 23: snprintf(out, cap, "TCP data offset greater than packet length"); break;
+    case 24: snprintf(out, cap, "Invalid TCP option length. Length %u less than 2", a0); break;
+    case 25: snprintf(out, cap, "Invalid TCP option length %u < 2", a0); break;
+    case 26: snprintf(out, cap, "Invalid TCP option length %u exceeds remaining %u bytes", a0, a1); break;
+    case 27: snprintf(out, cap, "Invalid UDP header. Length %u less than 8", a0); break;
+    case 28: snprintf(out, cap, "UDP packet too small: %u bytes", a0); break;
+    case 29: snprintf(out, cap, "vxlan packet too small"); break;
+    case 30: snprintf(out, cap, "ICMP layer less then 8 bytes for ICMPv4 packet"); break;
+    case 31: snprintf(out, cap, "LLC header too small"); break;
+    default: snprintf(out, cap, "gpd: unknown error code %u", code); break;
+  }
 }
 
 static int res_cmp(const char *what, const res_t *a, const res_t *b, uint64_t n) {
@@ -241,8 +312,8 @@ static int check_fragments(gpd_ctx *ctx, hipStream_t s, const gpd_batch *db, con
 }
 
 int main(int argc, char **argv) {
-  if (argc != 2) {
-    fprintf(stderr, "usage: %s BATCH_FILE\n", argv[0]);
+  if (argc != 2 && argc != 4) {
+    fprintf(stderr, "usage: %s BATCH_FILE [ERR_OUT PROTO_NAMES]\n", argv[0]);
     return 2;
   }
   FILE *f = fopen(argv[1], "rb");
@@ -272,7 +343,7 @@ int main(int argc, char **argv) {
 
   /* 1. device-resident batch on the caller's stream */
   res_t dv = res_alloc(n);
-  void *d_data, *d_off, *d_cap, *d_st, *d_ly, *d_nh, *d_th, *d_cs, *d_ho;
+  void *d_data, *d_off, *d_cap, *d_st, *d_ly, *d_nh, *d_th, *d_cs, *d_ho, *d_dt;
   hipStream_t s;
   HCHECK(hipStreamCreate(&s));
   HCHECK(hipMalloc(&d_data, alloc));
@@ -284,13 +355,14 @@ int main(int argc, char **argv) {
   HCHECK(hipMalloc(&d_th, 8 * n + 8));
   HCHECK(hipMalloc(&d_cs, 4 * n + 4));
   HCHECK(hipMalloc(&d_ho, 4 * n + 4));
+  HCHECK(hipMalloc(&d_dt, sizeof(gpd_detail) * (n + 1)));
   HCHECK(hipMemcpy(d_data, data, alloc, hipMemcpyHostToDevice));
   HCHECK(hipMemcpy(d_off, off, 4 * n, hipMemcpyHostToDevice));
   HCHECK(hipMemcpy(d_cap, cap, 4 * n, hipMemcpyHostToDevice));
   gpd_batch db = {(const uint8_t *)d_data, data_len, (const uint32_t *)d_off,
                   (const uint32_t *)d_cap, n};
   gpd_result dr = {(uint32_t *)d_st, (uint64_t *)d_ly, (uint64_t *)d_nh, (uint64_t *)d_th,
-                   (uint32_t *)d_cs, NULL, (uint32_t *)d_ho};
+                   (uint32_t *)d_cs, NULL, (uint32_t *)d_ho, NULL, (gpd_detail *)d_dt};
   CHECK(gpd_decode(ctx, &db, &dr, s));
   CHECK(gpd_sync(ctx, s));
   HCHECK(hipMemcpy(dv.status, d_st, 4 * n, hipMemcpyDeviceToHost));
@@ -299,36 +371,63 @@ int main(int argc, char **argv) {
   HCHECK(hipMemcpy(dv.tp_hash, d_th, 8 * n, hipMemcpyDeviceToHost));
   HCHECK(hipMemcpy(dv.csum, d_cs, 4 * n, hipMemcpyDeviceToHost));
   HCHECK(hipMemcpy(dv.hdr_off, d_ho, 4 * n, hipMemcpyDeviceToHost));
+  HCHECK(hipMemcpy(dv.detail, d_dt, sizeof(gpd_detail) * n, hipMemcpyDeviceToHost));
 
   /* 2. host batch through the library's pinned pipeline */
   res_t hv = res_alloc(n);
   gpd_batch hb = {data, data_len, off, cap, n};
-  gpd_result hr = {hv.status, hv.layers, hv.net_hash, hv.tp_hash, hv.csum, NULL, hv.hdr_off};
+  gpd_result hr = {hv.status, hv.layers, hv.net_hash, hv.tp_hash, hv.csum, NULL, hv.hdr_off, NULL, hv.detail};
   CHECK(gpd_decode_host(ctx, &hb, &hr));
 
   /* 3. the oracle */
   res_t ov = res_alloc(n);
+  gpd_ext_rec *oext = calloc(n + 1, sizeof(gpd_ext_rec));
   uint16_t *et = malloc(65536 * 2), *ip = malloc(256 * 2), *tp = malloc(65536 * 2),
            *up = malloc(65536 * 2);
   gpd_default_tables(et, ip, tp, up);
   gpo_tables t = {et, ip, tp, up};
   gpo_decode_batch(data, off, cap, n, GPD_LT_ETHERNET, cfg.decoders, cfg.options, &t, ov.status,
-                   ov.layers, ov.net_hash, ov.tp_hash, ov.csum, ov.hdr_off, NULL, 8);
+                   ov.layers, ov.net_hash, ov.tp_hash, ov.csum, ov.hdr_off, oext, 8);
 
   /* 4. the same packets as a pcap capture */
   res_t pv = res_alloc(n);
   uint64_t plen = 0, pn = 0, pnext = 0;
   int pstop = -1;
   uint8_t *cap_file = make_pcap(data, off, cap, n, &plen);
-  gpd_result pr = {pv.status, pv.layers, pv.net_hash, pv.tp_hash, pv.csum, NULL, pv.hdr_off};
+  gpd_result pr = {pv.status, pv.layers, pv.net_hash, pv.tp_hash, pv.csum, NULL, pv.hdr_off, NULL, pv.detail};
   CHECK(gpd_decode_pcap(ctx, cap_file, plen, n, &pr, &pn, &pnext, &pstop, 4));
   int bad = res_cmp("gpd_decode vs oracle", &dv, &ov, n) | res_cmp("gpd_decode_host vs oracle", &hv, &ov, n);
+  if (!bad) bad = detail_cmp("gpd_decode detail vs oracle", &dv, oext, n) |
+                  detail_cmp("gpd_decode_host detail vs oracle", &hv, oext, n);
   if (pn != n || pnext != plen || (n > 0 && pstop != GPD_PCAP_STOP_LIMIT && pstop != GPD_PCAP_STOP_EOF)) {
     fprintf(stderr, "gpd_decode_pcap: n %llu/%llu next %llu/%llu stop %d\n", (unsigned long long)pn,
             (unsigned long long)n, (unsigned long long)pnext, (unsigned long long)plen, pstop);
     bad = 1;
   } else {
     bad |= res_cmp("gpd_decode_pcap vs oracle", &pv, &ov, n);
+    if (!bad) bad |= detail_cmp("gpd_decode_pcap detail vs oracle", &pv, oext, n);
+  }
+
+  /* the error values, rebuilt from the device's status + detail words only */
+  if (!bad && argc >= 4) {
+    static char names[256][64];
+    FILE *nf = fopen(argv[3], "r");
+    if (!nf) { perror(argv[3]); return 2; }
+    for (int p = 0; p < 256; p++) {
+      if (!fgets(names[p], sizeof names[p], nf)) { fprintf(stderr, "short names file\n"); return 2; }
+      names[p][strcspn(names[p], "\n")] = 0;
+    }
+    fclose(nf);
+    FILE *ef = fopen(argv[2], "w");
+    if (!ef) { perror(argv[2]); return 2; }
+    char text[256];
+    for (uint64_t i = 0; i < n; i++) {
+      if (GPD_STATUS_CLASS(dv.status[i]) != GPD_ST_DECODE_ERROR) continue;
+      error_text(text, sizeof text, GPD_STATUS_ERRCODE(dv.status[i]), dv.detail[i].err_arg0,
+                 dv.detail[i].err_arg1, names);
+      fprintf(ef, "%llu\t%s\n", (unsigned long long)i, text);
+    }
+    fclose(ef);
   }
 
   /* 5. the device results feed the flow table */

@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol():
     lib = C.CDLL(_lib.LIB_PATH)
     missing = [f for f in declared_functions() if not hasattr(lib, f)]
     assert not missing, missing
-    assert lib.gpd_abi_version() == 6
+    assert lib.gpd_abi_version() == 7
 
 
 def test_python_binding_covers_the_header():
@@ -107,6 +107,14 @@ def test_c_host_program_on_the_abi(tmp_path):
     pkts += [mixed.packet(i) for i in range(mixed.n)]
     import test_defrag as TD  # the ip4defrag fixtures and fragment fuzz frames
     pkts += list(TD._frames().values()) + [f for _, f in TD.struct_frames()] + TD.fuzz_frames(600, 5)
+    import error_sites as ES
+    import errpath_cases as EC
+    import oracle_ref as O
+    from gopacket_amd.layers import ip_protocol_name
+    pkts += [bytes.fromhex(c["hex"]) for c in EC.load()]
+    pkts += ES.packets()
+    names = tmp_path / "ipproto_names.txt"
+    names.write_text("".join(ip_protocol_name(p) + "\n" for p in range(256)))
     for decoders, options in ((0xFFF, 0), (0x3FF, 1), (0x1 | 0x4 | 0x400 | 0x20 | 0x40 | 0x100, 0)):
         b = PacketBatch.from_packets(pkts)
         f = tmp_path / f"batch_{decoders:x}_{options}.bin"
@@ -116,12 +124,23 @@ def test_c_host_program_on_the_abi(tmp_path):
             fh.write(b.data[:b.data_len].tobytes())
             fh.write(b.offset.astype(np.uint32).tobytes())
             fh.write(b.caplen.astype(np.uint32).tobytes())
-        r = subprocess.run([exe, str(f)], capture_output=True, text=True, timeout=90)
+        errs = tmp_path / f"errors_{decoders:x}_{options}.txt"
+        r = subprocess.run([exe, str(f), str(errs), str(names)], capture_output=True, text=True, timeout=90)
         assert r.returncode == 0, r.stdout + r.stderr
         words = r.stdout.split()
         assert words[:3] == ["abi_host", "ok", str(b.n)], r.stdout
         assert int(words[3]) > 100, r.stdout  # the mixed traffic holds many TCP/UDP flows
         assert int(words[4]) > 100, r.stdout  # ip4defrag's fragments and the fuzz frames
+        # the C host's error texts (from status + gpd_detail) == the oracle's, packet by packet
+        ref = O.decode(b, 17, decoders, options, ext=True, nthreads=8)
+        want = {i: str(ref.err(i)) for i in range(b.n) if (int(ref.status[i]) & 3) == 2}
+        got = {}
+        for line in errs.read_text().splitlines():
+            i, text = line.split("\t", 1)
+            got[int(i)] = text
+        assert got == want
+        if decoders == 0xFFF:  # every decoder registered: every error site of gpd.h is reached
+            assert {int(ref.status[i]) >> 9 & 63 for i in want} == set(range(1, 32))
 
 
 def test_integration_build_command_names_every_source():

@@ -54,6 +54,37 @@ def assert_same(dev, ref, batch=None, ext=True):
             i = int(bad[0])
             raise AssertionError(f"ext differs at {len(bad)} packets; first i={i}: dev={dev.ext[i]} "
                                  f"ref={ref.ext[i]}")
+    if getattr(dev, "detail", None) is not None and ref.ext is not None:
+        assert_detail(dev, ref)
+
+
+def detail_rows(st):
+    """Packets whose gpd_detail record the kernel writes: decode errors, > 12 layers."""
+    st = st.astype(np.uint32)
+    return np.nonzero(((st & 3) == 2) | (((st >> 4) & 31) > 12) | (((st >> 3) & 1) == 1))[0]
+
+
+def assert_detail(dev, ref, texts=True):
+    """dev.detail (written by the generic decoder, fast path or not) == the oracle's ext prefix for
+    every packet that has one; and the error values / decoded lists rebuilt from the core words +
+    detail alone equal the oracle's."""
+    rows = detail_rows(ref.status)
+    a = dev.detail.view(np.uint8).reshape(len(dev), -1)[rows]
+    b = ref.ext.view(np.uint8).reshape(len(ref), -1)[rows, :24]
+    bad = np.nonzero(np.any(a != b, axis=1))[0]
+    if len(bad):
+        i = int(rows[bad[0]])
+        raise AssertionError(f"detail differs at {len(bad)} packets; first i={i}: dev={dev.detail[i]} "
+                             f"ref={ref.ext[i]['layer_codes']} {ref.ext[i]['err_arg0']} {ref.ext[i]['err_arg1']}")
+    if texts:
+        ext, dev.ext = dev.ext, None  # (the core words + detail only)
+        try:
+            for i in rows[:4096]:
+                i = int(i)
+                assert str(dev.err(i)) == str(ref.err(i)), (i, str(dev.err(i)), str(ref.err(i)))
+                assert dev.decoded(i) == ref.decoded(i), i
+        finally:
+            dev.ext = ext
 
 
 def run_both(batch, first=L.LayerTypeEthernet, mask=ALL, options=0, tables=None, ext=True,
@@ -71,6 +102,29 @@ def run_both(batch, first=L.LayerTypeEthernet, mask=ALL, options=0, tables=None,
         out = out or dev
     return out  # the ext result when ext records were asked for
     return dev
+
+
+def test_error_sites_detail_and_texts():
+    """One packet per reference error site (tests/error_sites.py, pinned on the oracle by
+    tests/test_error_sites.py) and > 12-layer stacks, mixed into fast-path traffic: without ext
+    (fast kernel, each failing packet decoded by its wave's fallback list) and with ext (generic
+    kernel), the detail records and the texts rebuilt from them equal the oracle's.  The same
+    batch through gpd_decode_host fills detail as well."""
+    import error_sites as ES
+    bulk = synth.make_udp64(4096)
+    pk = [bulk.packet(i) for i in range(bulk.n)]
+    sites = ES.packets()
+    for k, p in enumerate(sites):  # spread among the fast-path packets
+        pk.insert(37 * k + 5, p)
+    b = PacketBatch.from_packets(pk)
+    for opts in (0, 1):
+        dev = run_both(b, L.LayerTypeEthernet, ALL, opts)
+        ref = O.decode(b, L.LayerTypeEthernet, ALL, opts, ext=True, nthreads=8)
+        rows = detail_rows(ref.status)
+        assert len(rows) == len(sites)
+        assert {int(ref.status[i]) >> 9 & 63 for i in rows} >= set(range(1, 32))
+        host = _parser(options=opts).DecodeBatchHost(b, detail=True)
+        assert_same(host, ref, b, ext=False)
 
 
 META = G.load()
@@ -416,24 +470,30 @@ def _oracle_threads() -> int:
     return max(1, min(n, 64))
 
 
+BENCH_MASK = 0x3FF  # the decoder set bench.py times (bench.py: Ethernet .. Fragment, no ICMPv4 / LLC)
+
+
 def _full_size_exact(b):
     """Every packet of a full-size batch, all five result words and hdr_off, in the gpd_record
-    (AoS) form the bench times and in the SoA form, against the multi-threaded oracle.  Returns
-    the SoA result for the property checks."""
+    (AoS) form and in the SoA form, against the multi-threaded oracle — with the decoder set the
+    bench times `value` on (BENCH_MASK) and with every decoder.  Returns the last SoA result for
+    the property checks."""
     import torch
     from gopacket_amd import parser as P
-    ref = O.decode(b, L.LayerTypeEthernet, ALL, 0, ext=False, nthreads=_oracle_threads())
-    p = _parser()
     db = P.DeviceBatch(b, 0)
     res = None
-    for records in (True, False):
-        dr = P.DeviceResult(b.n, 0, hdr_off=True, records=records)
-        p.decode_device(db, dr)
-        torch.cuda.synchronize()
-        res = dr.to_host()
-        del dr
-        assert_same(res, ref, b, ext=False)
-    del db, ref
+    for mask in (BENCH_MASK, ALL):
+        ref = O.decode(b, L.LayerTypeEthernet, mask, 0, ext=False, nthreads=_oracle_threads())
+        p = _parser(mask=mask)
+        for records in (True, False):
+            dr = P.DeviceResult(b.n, 0, hdr_off=True, records=records)
+            p.decode_device(db, dr)
+            torch.cuda.synchronize()
+            res = dr.to_host()
+            del dr
+            assert_same(res, ref, b, ext=False)
+        del ref
+    del db
     torch.cuda.empty_cache()
     return res
 
