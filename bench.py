@@ -576,6 +576,53 @@ REPLAY_CHUNK = 1 << 24   # records per device index chunk and per gpd_decode_pca
 REPLAY_SEED = 0x5EED0002
 
 
+def host_placement(arr, local: int) -> dict:
+    """Where a large host buffer's pages sit (diagnostic of the PCIe-inclusive leg): its NUMA
+    nodes (pages per node, /proc/self/numa_maps), how much of it transparent huge pages back
+    (AnonHugePages, /proc/self/smaps) and the GPU's own NUMA node (sysfs, by PCI bus id)."""
+    out = {}
+    lo = arr.ctypes.data
+    hi = lo + arr.nbytes
+    try:
+        nodes = {}
+        with open("/proc/self/numa_maps") as f:
+            for line in f:
+                a = int(line.split()[0], 16)
+                if lo - (1 << 21) <= a < hi:
+                    for tok in line.split()[1:]:
+                        if tok[0] == "N" and "=" in tok:
+                            k, v = tok.split("=")
+                            nodes[k] = nodes.get(k, 0) + int(v)
+        out["numa_pages"] = nodes
+    except (OSError, ValueError):
+        pass
+    try:
+        huge, rss, cur = 0, 0, None
+        with open("/proc/self/smaps") as f:
+            for line in f:
+                head = line.split()[0]
+                if "-" in head and not head.endswith(":"):
+                    a, b = (int(x, 16) for x in head.split("-"))
+                    cur = a < hi and b > lo
+                elif cur and head == "AnonHugePages:":
+                    huge += int(line.split()[1])
+                elif cur and head == "Rss:":
+                    rss += int(line.split()[1])
+        out["rss_kB"], out["anon_huge_kB"] = rss, huge
+    except (OSError, ValueError):
+        pass
+    try:
+        import torch
+        pr = torch.cuda.get_device_properties(local)
+        bus = f"{getattr(pr, 'pci_domain_id', 0):04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
+        out["gpu_pci"] = bus
+        with open(f"/sys/bus/pci/devices/{bus}/numa_node") as f:
+            out["gpu_numa_node"] = int(f.read().strip())
+    except Exception:  # noqa: BLE001 (diagnostic only)
+        pass
+    return out
+
+
 def shm_fits(nbytes: int) -> bool:
     st = os.statvfs("/dev/shm")
     return st.f_bavail * st.f_frsize >= nbytes
@@ -852,27 +899,44 @@ def bench_replay(args, world, rank, local, dist):
     st = (res.records.view(torch.int32)[0::8] if aos else res.status).cpu().numpy().view(np.uint32)
     n_err = int(np.count_nonzero((st & 3) != 0))
     # PCIe-inclusive leg: the shard streamed from host memory in 2^24-record calls
-    z = lambda dt: np.zeros(REPLAY_CHUNK, dt)
+    call = args.pcie_call_records or REPLAY_CHUNK  # records per gpd_decode_pcap_at call
+    z = lambda dt: np.zeros(call, dt)
     out = BatchResult(z(np.uint32), z(np.uint64), z(np.uint64), z(np.uint64), z(np.uint32), None,
                       z(np.uint32))
     # a capture loop keeps its result arrays: registered, the results land in them by DMA
     outs = [out.status, out.layers, out.net_hash, out.tp_hash, out.csum, out.hdr_off]
     for a in outs:
         check(lib.gpd_host_register(h, a.ctypes.data, a.nbytes), "gpd_host_register")
-    parser.DecodePcapAt(cap, info, start, min(REPLAY_CHUNK, m), out, threads, data_len=end)  # warm
+    parser.DecodePcapAt(cap, info, start, min(call, m), out, threads, data_len=end)  # warm
     if dist:
         dist.barrier()
+    # where the time of the PCIe-inclusive leg goes: each call's wall time and its phases
+    # (gpd_decode_pcap_last_times: walk, staging, waits for the slots' transfers + decode, drain)
+    call_ms, phases = [], np.zeros(6, np.float64)
+    ph = np.zeros(6, np.float64)
     t0 = time.perf_counter()
     p, done, last = start, 0, 0
     while done < m:
-        k, p, stop, err = parser.DecodePcapAt(cap, info, p, min(REPLAY_CHUNK, m - done), out, threads,
+        tc = time.perf_counter()
+        k, p, stop, err = parser.DecodePcapAt(cap, info, p, min(call, m - done), out, threads,
                                               data_len=end)
+        call_ms.append((time.perf_counter() - tc) * 1e3)
+        lib.gpd_decode_pcap_last_times(ph.ctypes.data)
+        phases += ph
         assert err is None and k > 0, err
         done += k
         last = k
     if dist:
         dist.barrier()
     t_pcie = time.perf_counter() - t0
+    cm = np.array(call_ms)
+    pcie_diag = {"calls": len(call_ms), "call_ms_median": round(float(np.median(cm)), 3),
+                 "call_ms_min": round(float(cm.min()), 3), "call_ms_max": round(float(cm.max()), 3),
+                 "call_ms_first4": [round(float(x), 3) for x in cm[:4]],
+                 "call_ms_by_quarter": [round(float(q.mean()), 3) for q in np.array_split(cm, 4) if len(q)],
+                 "phases_ms_total": dict(zip(["total", "walk", "walk_wait", "stage", "sync", "drain"],
+                                             [round(float(x), 1) for x in phases])),
+                 "capture_placement": host_placement(cap, local)}
     # the streamed results of the last call equal the resident ones for the same records
     tail = res.fields(m - last, m)
     same = all(np.array_equal(getattr(out, f)[:last], tail[f])
@@ -934,11 +998,13 @@ def bench_replay(args, world, rank, local, dist):
                      "read_frac_per_rank": [x["read_frac"] for x in per_rank]},
         "pcie_inclusive": {"Mpackets_per_s": round(n / pcie_max / 1e6, 1), "s": round(pcie_max, 3),
                            "GBps_capture_in": round(dl / pcie_max / 1e9, 2),
-                           "path": "registered shared capture -> gpd_decode_pcap_at per 2^24 records "
+                           "records_per_call": call,
+                           "path": "registered capture -> gpd_decode_pcap_at per call "
                                    "(raw bytes H2D in 64 MiB chunks, records found in HBM by the "
                                    "device walk, decode, results D2H into registered result "
                                    "arrays)"},
         "per_rank": per_rank,
+        "pcie_diag_rank0": pcie_diag,
         "setup_s": {"generate": round(rows[0][7], 2), "locate": round(rows[0][8], 2),
                     "register": round(rows[0][9], 2), "h2d": round(rows[0][10], 2),
                     "index": round(rows[0][11], 2)},
@@ -1003,6 +1069,8 @@ def main():
     ap.add_argument("--packets", type=int, default=0, help="override packets per GPU (replay: "
                     "records in the whole capture, default 10^9)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pcie-call-records", type=int, default=0,
+                    help="config 5 PCIe-inclusive leg: records per gpd_decode_pcap_at call (default 2^24)")
     ap.add_argument("--no-side", action="store_true", help="skip the other configurations' "
                     "figures (tcp64, imix, vxlan, pcap64) the default udp64 line carries")
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU-baseline timing "

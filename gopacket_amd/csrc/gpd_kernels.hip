@@ -48,13 +48,15 @@ constexpr uint32_t kDiagNtStore = 1u << 28;     // A/B: result stores with the n
 constexpr uint32_t kShiftWindows = 1u << 27;    // internal: register-staged windows copied shifted
 constexpr uint32_t kRegPrefix = 1u << 26;       // internal: 8 KiB windows of long frames (IMIX)
 constexpr uint32_t kHeaderOnce = 1u << 25;      // internal: 8 KiB windows decoded once per tile (seg_pass)
+constexpr uint32_t kRounds = 1u << 24;          // internal: header-once over 8 KiB rounds (ro_kernel)
 constexpr uint32_t kDiagMask = kDiagSkipDecode | kDiagNoWait | kDiagNtLoad | kDiagNtStore | kShiftWindows |
-                               kRegPrefix | kHeaderOnce;
-// A/B builds only (GPD_EXTRA_CFLAGS=-DGPD_EXP=..., tools/ab_exp.sh): fast-path variants
+                               kRegPrefix | kHeaderOnce | kRounds;
+// A/B builds only (GPD_EXTRA_CFLAGS=-DGPD_EXP=..., tools/ab_exp.sh): a fast-path variant under
+// test reads kExp inside an `#if GPD_EXP` block; the shipped library has none.
 #ifndef GPD_EXP
 #define GPD_EXP 0
 #endif
-[[maybe_unused]] constexpr uint32_t kExp = GPD_EXP;  // (no variant under test)
+[[maybe_unused]] constexpr uint32_t kExp = GPD_EXP;
 
 extern __shared__ __attribute__((aligned(16))) uint8_t g_lds[];
 
@@ -939,21 +941,20 @@ __device__ __forceinline__ uint32_t seg_sum_chunks(uint32_t S, uint32_t len, uin
   return s;
 }
 
-// seg_pass: the first round trip of fast_decode (the Ethernet and network header bytes) kept
-// in h, and the segment that fast_decode's guesses lead to (IPv4 IHL 5 / IPv6 by the version
-// nibble, TCP / UDP by the protocol number, UDP Length) summed from this window: its head
-// and tail here, the whole chunks between left to the window's chunk prefix sums (sg) when it
-// is long and even-aligned.  fast_decode<HO> confirms the guesses with the dispatch tables and
-// uses the sum only when its own transport segment is exactly h.pos (else the packet takes
-// the generic decoder).  With VXLAN registered (vxreg), a UDP segment whose ports lead to it
-// is flagged (h.ok = 2) for the full decode in this window: its inner headers are not staged.
-template <bool COOP>
-__device__ __forceinline__ void seg_pass(uint32_t p, uint32_t len, uint32_t buf, Hdr &h, Seg &sg,
-                                         const FastCtx &F, bool vxreg) {
+// hdr_parse: the first round trip of fast_decode (the Ethernet and network header bytes) kept
+// in h, and the transport segment that fast_decode's guesses lead to (IPv4 IHL 5 / IPv6 by the
+// version nibble, TCP / UDP by the protocol number, UDP Length): h.pos and (l4, seg); false
+// when there is none.  Reads the packet's first 128 bytes at most (a TCP options walk).
+// fast_decode<HO> confirms the guesses with the dispatch tables and uses the segment's sum only
+// when its own transport segment is exactly h.pos (else the packet takes the generic decoder).
+// With VXLAN registered (vxreg), a UDP segment whose ports lead to it is flagged (h.ok = 2) for
+// the full decode in the window that holds it: its inner headers are not staged.
+__device__ __forceinline__ bool hdr_parse(uint32_t p, uint32_t len, Hdr &h, const FastCtx &F, bool vxreg,
+                                          uint32_t &l4_out, uint32_t &seg_out) {
   h.pos = 0xFFFFFFFFu;
   h.sum = 0;
   h.ok = 0;
-  if (len < 15u) return;
+  if (len < 15u) return false;
   const U128 e = ld128(p + 8);
   h.e1 = e.y;
   h.e2 = e.z;
@@ -962,8 +963,8 @@ __device__ __forceinline__ void seg_pass(uint32_t p, uint32_t len, uint32_t buf,
   const uint32_t t1 = tag_type(et0), t2 = t1 & tag_type(et1);
   const uint32_t l3 = 14 + 4 * (t1 + t2);
   load64(h.W, p + l3);  // one trip after the tags are known (no speculative untagged read)
-  if (et0 < 0x0600u) return;
-  if (len < l3 + 20u) return;
+  if (et0 < 0x0600u) return false;
+  if (len < l3 + 20u) return false;
   const uint32_t *W = h.W;
   const uint32_t ver = (W[0] >> 4) & 15u;
   const bool v4 = ver == 4u;
@@ -971,15 +972,15 @@ __device__ __forceinline__ void seg_pass(uint32_t p, uint32_t len, uint32_t buf,
   const uint32_t length = v4 ? be_hi(W[0]) : be_lo(W[1]);
   uint32_t plen;
   if (v4) {
-    if ((W[0] & 0x0Fu) != 5u || length < 20u) return;
+    if ((W[0] & 0x0Fu) != 5u || length < 20u) return false;
     plen = (dl > length ? length : dl) - 20u;
   } else {
-    if (ver != 6u || dl < 40u) return;
+    if (ver != 6u || dl < 40u) return false;
     plen = (length > dl - 40u) ? dl - 40u : length;
   }
   const uint32_t proto = v4 ? ((W[2] >> 8) & 0xFFu) : ((W[1] >> 16) & 0xFFu);
   const uint32_t g = proto == 6u ? 1u : (proto == 17u ? 2u : 0u);
-  if (!g) return;
+  if (!g) return false;
   const uint32_t ty = v4 ? W[6] : W[11], tw = v4 ? W[8] : W[13];
   const uint32_t l4 = l3 + (v4 ? 20u : 40u);
   const uint32_t ulen = be_lo(ty);
@@ -990,7 +991,7 @@ __device__ __forceinline__ void seg_pass(uint32_t p, uint32_t len, uint32_t buf,
     const uint32_t rs = fix_bucket_at(kFixUdpBase, F.mult, be_lo(tx));
     if ((ports_next_raw(rd, rs, F.pl_raw) & 15u) == D_VXLAN) {
       h.ok = 2;
-      return;
+      return false;
     }
   }
   if (g == 1u) {  // the options walk of fast_decode, on the guess
@@ -1010,6 +1011,19 @@ __device__ __forceinline__ void seg_pass(uint32_t p, uint32_t len, uint32_t buf,
     h.ok = ok;
   }
   h.pos = l4 | (seg << 16);
+  l4_out = l4;
+  seg_out = seg;
+  return true;
+}
+
+// seg_pass (the per-window header-once step): hdr_parse, and the transport segment it guessed
+// summed from this window: its head and tail here, the whole chunks between left to the
+// window's chunk prefix sums (sg) when it is long and even-aligned.
+template <bool COOP>
+__device__ __forceinline__ void seg_pass(uint32_t p, uint32_t len, uint32_t buf, Hdr &h, Seg &sg,
+                                         const FastCtx &F, bool vxreg) {
+  uint32_t l4, seg;
+  if (!hdr_parse(p, len, h, F, vxreg, l4, seg)) return;
   const uint32_t S = p + l4;
   if (COOP && seg >= 64u && !(S & 1u)) {
     // head [S, A) and tail [B, E) from their aligned chunks; [A, B) from the prefix sums
@@ -1059,7 +1073,15 @@ __device__ __forceinline__ void seg_pass(uint32_t p, uint32_t len, uint32_t buf,
 template <bool CS, bool HASH, bool COOP, bool HO = false, bool AL = false>
 __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const FastCtx &F, Out &o,
                                             uint32_t buf, Seg &sg, const Hdr *h = nullptr) {
+  // nh: the last network layer's NetworkFlow().FastHash() — in the two-pass decode, for IPv4 its
+  // two raw address words, hashed once at the end; tpx: the last transport's raw port word,
+  // likewise.  (A VXLAN frame's outer IPv4 and UDP layers are overwritten by its inner pass,
+  // A11: hashing them as they were accepted cost ~70 VALU per packet for nothing.  The one-pass
+  // header-once decode hashes as it accepts: deferred, the hashes' temporaries overlap and cost
+  // it ~30 VGPRs.)
+  constexpr bool DEFER_HASH = false;  // (measured: +20-45 VGPRs and spills at 3-4 waves per SIMD)
   uint64_t codes = 0, nh = 0, th = 0;
+  uint32_t tpx = 0;
   uint32_t nc = 0, trunc = 0, stop = 0;
   uint32_t net = 0, tp = 0, ip4 = 0, ipcs = 0;
   uint32_t tp_off = 0, tp_len = 0, tp_pl = 0;  // the last transport; its proto + length terms
@@ -1156,7 +1178,8 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
                            dot2(W[0], 0x00010001u, ps))));
         ip4 = 1;
       }
-      if (HASH) nh = flow_fast(fnv_start<4>(W[3]), fnv_start<4>(W[4]), 1u);  // ip4.go:63-65
+      if (HASH) nh = DEFER_HASH ? ((uint64_t)W[4] << 32) | W[3]  // ip4.go:63-65, hashed at the end
+                                : flow_fast(fnv_start<4>(W[3]), fnv_start<4>(W[4]), 1u);
       ps4 = ps;
       net = 1;
       net_off = l3;
@@ -1224,7 +1247,8 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
       put(GPD_C_UDP);
     }
     tp = g;
-    if (HASH) th = flow_fast(fnv_start<2>(tx), fnv_start<2>(tx >> 16), g == 1u ? 4u : 5u);
+    tpx = tx;  // tcp.go:331-333 / udp.go:123-125: the ports
+    if (HASH && !DEFER_HASH) th = flow_fast(fnv_start<2>(tx), fnv_start<2>(tx >> 16), g == 1u ? 4u : 5u);
     // pseudo-header protocol and length as LE-domain words (seg < 2^16 in a window); the
     // addresses are added at the end from the network object of this kind as the call
     // leaves it (SetNetworkLayerForChecksum(&ip4) reads the reused object: for VXLAN whose
@@ -1251,6 +1275,10 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
   }
 
   // ---- outputs, composed exactly as decode_packet does
+  if (HASH && DEFER_HASH) {
+    if (net == 1u) nh = flow_fast(fnv_start<4>((uint32_t)nh), fnv_start<4>((uint32_t)(nh >> 32)), 1u);
+    if (tp) th = flow_fast(fnv_start<2>(tpx), fnv_start<2>(tpx >> 16), tp == 1u ? 4u : 5u);
+  }
   const uint32_t tp_ps = tp_pl + (tp_kind == 1u ? ps4 : ps6);
   uint32_t st = (stop ? F.unsup : GPD_ST_OK) | (trunc << 2) | (nc << 4);
   uint32_t cs = 0;
@@ -1721,6 +1749,46 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void decode_kernel(KParams P) {
   }
 }
 
+// The end of a fast wave: its fallback list — the generic DecodingLayerParser loop
+// (decode_packet), one lane per listed packet, its bytes read from global memory — here, at the
+// end of the wave, overlapped with the other waves' streaming.  (A second kernel over the lists
+// cost a launch boundary, ~5 us per launch, even when every list is empty.)  The live state of
+// the streaming loop is dead by now, so the generic decoder's registers do not raise the
+// kernel's.  Each round first stages every listed packet's first K bytes in the lane's slot of
+// the (now idle) window buffer `buf` with independent 16-byte loads, so the decoder's dependent
+// header reads hit LDS (HybSrc); bytes past the slot (long segments) still come from global
+// memory.
+template <uint32_t K>
+__device__ __forceinline__ void decode_fallback_list(const KParams &P, uint32_t buf, uint32_t fb_start, uint32_t fb_c,
+                                                     uint32_t lane, uint32_t dlen, uint32_t options) {
+  if (fb_c) {
+    __threadfence_block();  // the entries other lanes of this wave stored
+    const Tab<false> T{P.pages,    P.eth_base, P.tcp_base, P.udp_base, P.eth_bits,
+                       P.tcp_bits, P.udp_bits, P.eth_mult, P.tcp_mult, P.udp_mult};
+    const uint32_t slot = buf + K * lane;
+    // readable bound of the batch contract (gpd.h gpd_batch: round_up(data_len, 16)): every
+    // 16-byte chunk below it is whole, so no staging load reaches past it
+    const uint64_t rlim = ((uint64_t)dlen + 15u) & ~15ull;
+    for (uint32_t j = lane; j - lane < fb_c; j += 64u) {
+      const bool live = j < fb_c;
+      const uint32_t fi = live ? P.fb_list[fb_start + j] : 0u;
+      const uint32_t off = live ? min(P.offset[fi], dlen) : 0u;
+      const uint32_t len = live ? min(P.caplen[fi], dlen - off) : 0u;
+      const uint64_t gb = (uint64_t)off & ~15ull;
+      v4u32 c[K / 16u];
+#pragma unroll
+      for (uint32_t k = 0; k < K / 16u; k++)
+        c[k] = (live && gb + 16u * k < rlim) ? *reinterpret_cast<const v4u32 *>(P.data + gb + 16u * k)
+                                              : v4u32{0u, 0u, 0u, 0u};
+#pragma unroll
+      for (uint32_t k = 0; k < K / 16u; k++) *reinterpret_cast<v4u32 *>(g_lds + slot + 16u * k) = c[k];
+      if (live)
+        store_out(P, fi, decode_packet<false>(HybSrc<K>{P.data, off, gb, slot}, len, T, P.first, options, nullptr,
+                                              P.detail ? P.detail + fi : nullptr));
+    }
+  }
+}
+
 // ---------------------------------------------------------------- register-staged fast loop
 
 // LDS bytes per wave of rs_kernel: one window (the next one waits in VGPRs), plus the chunk
@@ -2027,7 +2095,7 @@ __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
                                                __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = i;
         fb_c += (uint32_t)__popcll(m);
       }
-      const uint32_t keep = (kExp & 4u) ? valid_d : (valid_d && !fb);  // a listed packet is stored once, by its decode below
+      const uint32_t keep = valid_d && !fb;  // a listed packet is stored once, by its decode below
       fb = 0;
       if (DEFER) {
         st_pending = true;
@@ -2058,46 +2126,293 @@ __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
     cov_d = cov_n;
   }
   if (lane == 0u) P.fb_wcount[gw] = fb_c;  // (gpd_last_launch_split's count)
-  // This wave's fallback list: the generic DecodingLayerParser loop (decode_packet), one lane per
-  // listed packet, its bytes read from global memory — here, at the end of the wave, overlapped
-  // with the other waves' streaming.  (A second kernel over the lists cost a launch boundary,
-  // ~5 us per launch, even when every list is empty.)  The live state of the loop above is dead
-  // by now, so the generic decoder's registers do not raise the kernel's.
-  // Each round first stages every listed packet's first STAGE/64 bytes in the lane's slot of the
-  // (now idle) window buffer with independent 16-byte loads, so the decoder's dependent header
-  // reads hit LDS (HybSrc); bytes past the slot (long segments) still come from global memory.
-  if (!(kExp & 8u) && fb_c) {
-    __threadfence_block();  // the entries other lanes of this wave stored
-    const Tab<false> T{P.pages,    P.eth_base, P.tcp_base, P.udp_base, P.eth_bits,
-                       P.tcp_bits, P.udp_bits, P.eth_mult, P.tcp_mult, P.udp_mult};
-    constexpr uint32_t K = (uint32_t)STAGE / 64u;
-    const uint32_t slot = buf + K * lane;
-    // readable bound of the batch contract (gpd.h gpd_batch: round_up(data_len, 16)): every
-    // 16-byte chunk below it is whole, so no staging load reaches past it
-    const uint64_t rlim = ((uint64_t)dlen + 15u) & ~15ull;
-    for (uint32_t j = lane; j - lane < fb_c; j += 64u) {
-      const bool live = j < fb_c;
-      const uint32_t fi = live ? P.fb_list[fb_start + j] : 0u;
-      const uint32_t off = live ? min(P.offset[fi], dlen) : 0u;
-      const uint32_t len = live ? min(P.caplen[fi], dlen - off) : 0u;
-      const uint64_t gb = (uint64_t)off & ~15ull;
-      if (!(kExp & 128u)) {
-        v4u32 c[K / 16u];
+  decode_fallback_list<(uint32_t)STAGE / 64u>(P, buf, fb_start, fb_c, lane, dlen, options);
+}
+
+// ---------------------------------------------------------------- round-based header-once loop
+// ro_kernel (gpd_tuning.header_once = 2): the header-once decode of long frames, with each
+// 64-packet tile's bytes streamed as ONE contiguous run in rounds of 8 KiB — the traffic shape
+// of the attainable probe — instead of windows cut at packet boundaries (IMIX: 3.35 windows of
+// 6.8 KiB per 22.7-KiB tile, 21 % of each window's loads re-reading its first chunk).
+//  * A packet's header (its first <= 128 bytes) is staged in the round that holds them; the
+//    previous round's last 144 bytes stay in front of the window, so a header may straddle the
+//    boundary.
+//  * Its transport segment [S, E) is summed from the tile's running chunk prefix sums G: the
+//    masked head chunk and G(A) where the header is staged, G(B) and the masked tail chunk in
+//    the round that holds B (A = S rounded up, B = E rounded down to 16) — one compare per
+//    pending lane per round until then.  So a segment may span any number of rounds, and a
+//    packet larger than a window stays on the fast path.  An odd-aligned segment is summed in
+//    the other byte order (RFC 1071 §2(B)) and swapped back.
+//  * The straight-line decode runs once per tile from the staged headers (fast_decode<HO>).
+//  * A tile whose packets do not lie nearly back to back (a shuffled or scattered layout: the
+//    run much longer than its bytes) is left to the generic decoder whole.
+constexpr uint32_t kRoStage = 8192;
+constexpr uint32_t kRoCarry = 144;    // bytes of the previous round kept in front of the window
+constexpr uint32_t kRoPfxCarry = 12;  // prefix words kept in front of the prefix array (9 used)
+constexpr uint32_t kRoHdr = 128;      // header bytes a packet's staging (hdr_parse) reads at most
+__host__ __device__ constexpr uint32_t ro_wave_lds_bytes() {
+  return kRoCarry + kRoStage + 16u + 4u * kRoPfxCarry + 4u * (kRoStage / 16u + 1u) + 12u;
+}
+static_assert(ro_wave_lds_bytes() % 16u == 0u, "ro_kernel: 16-byte aligned wave regions");
+
+// LE-domain sum s + bytes [lo, hi) of the aligned 16-byte LDS chunk at a (0 <= lo <= hi <= 16).
+__device__ __forceinline__ uint32_t chunk_part(uint32_t a, uint32_t lo, uint32_t hi, uint32_t s) {
+  const uint4 q = *reinterpret_cast<const uint4 *>(g_lds + a);
+  const uint32_t l8 = lo * 8u, h8 = hi * 8u;
+  const uint64_t keep_lo = (l8 >= 64u ? 0ull : ~0ull << l8) & (h8 >= 64u ? ~0ull : (1ull << h8) - 1ull);
+  const uint64_t keep_hi = (l8 >= 64u ? ~0ull << (l8 - 64u) : ~0ull) &
+                           (h8 <= 64u ? 0ull : (h8 >= 128u ? ~0ull : (1ull << (h8 - 64u)) - 1ull));
+  const uint64_t x = ((((uint64_t)q.y << 32) | q.x) & keep_lo), y = ((((uint64_t)q.w << 32) | q.z) & keep_hi);
+  s = dot2((uint32_t)x, 0x00010001u, s);
+  s = dot2((uint32_t)(x >> 32), 0x00010001u, s);
+  s = dot2((uint32_t)y, 0x00010001u, s);
+  return dot2((uint32_t)(y >> 32), 0x00010001u, s);
+}
+
+// min / sum over the wave (all 64 lanes take part)
+__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
 #pragma unroll
-        for (uint32_t k = 0; k < K / 16u; k++)
-          c[k] = (live && gb + 16u * k < rlim) ? *reinterpret_cast<const v4u32 *>(P.data + gb + 16u * k)
-                                                : v4u32{0u, 0u, 0u, 0u};
+  for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o));
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 #pragma unroll
-        for (uint32_t k = 0; k < K / 16u; k++) *reinterpret_cast<v4u32 *>(g_lds + slot + 16u * k) = c[k];
-        if (live)
-          store_out(P, fi, decode_packet<false>(HybSrc<K>{P.data, off, gb, slot}, len, T, P.first, options, nullptr,
-                                                P.detail ? P.detail + fi : nullptr));
-      } else if (live) {
-        store_out(P, fi, decode_packet<false>(GlbSrc{P.data, off}, len, T, P.first, options, nullptr,
-                                              P.detail ? P.detail + fi : nullptr));
+  for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
+  return v;
+}
+
+template <bool CS, bool HASH, int MINW>
+__global__ __launch_bounds__(256, MINW) void ro_kernel(KParams P) {
+  constexpr int WAVES = 4;
+  constexpr int NC = (int)kRoStage / 1024;  // 16-byte chunks per lane per round
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  for (uint32_t k = threadIdx.x; k < P.image_words; k += 64 * WAVES)
+    reinterpret_cast<uint32_t *>(g_lds)[k] = P.image[k];
+  __syncthreads();
+  const uint32_t img = (P.image_words * 4u + 15u) & ~15u;
+  const uint32_t buf = img + wave * ro_wave_lds_bytes() + kRoCarry;  // the round's window
+  const uint32_t pfx = buf + kRoStage + 16u + 4u * kRoPfxCarry;      // its chunk prefix sums P[0..512]
+  const uint32_t n = P.n_dev ? min((uint32_t)P.n, *P.n_dev) : (uint32_t)P.n;
+  const uint32_t ntiles = (n + 63u) >> 6;
+  const uint32_t nwaves = gridDim.x * WAVES;
+  const uint32_t dlen = (uint32_t)P.data_len;
+  const uint32_t options = P.options & ~kDiagMask;
+  const FastCtx F{P.eth_mult, ((uint32_t)GPD_LT_PAYLOAD << 8) | (reinterpret_cast<const uint8_t *>(g_lds)[GPD_LT_PAYLOAD]),
+                  (options & GPD_OPT_IGNORE_UNSUPPORTED) ? GPD_ST_OK : GPD_ST_UNSUPPORTED,
+                  reinterpret_cast<const uint8_t *>(g_lds)[GPD_LT_FRAGMENT]};
+  const bool vxreg = (P.decoders & GPD_DEC_VXLAN) != 0;
+
+  uint32_t tp = blockIdx.x * WAVES + wave;  // the planner's tile
+  const uint32_t gw = tp;  // this wave's fallback region (see rs_kernel)
+  const uint32_t fb_start = 64u * (gw * (ntiles / nwaves) + min(gw, ntiles % nwaves));
+  uint32_t fb_c = 0;
+  if (tp >= ntiles) {
+    if (lane == 0u) P.fb_wcount[gw] = 0u;
+    return;
+  }
+  auto dload = [&](uint32_t u, uint32_t &o, uint32_t &c) {  // descriptors of tile u
+    const uint32_t i = u * 64u + lane;
+    o = c = 0;
+    if (u < ntiles && i < n) {
+      o = __builtin_nontemporal_load(P.offset + i);
+      c = __builtin_nontemporal_load(P.caplen + i);
+    }
+  };
+  auto dread = [&](uint32_t u, uint32_t o_raw, uint32_t c_raw, uint32_t &off, uint32_t &end) -> uint32_t {
+    const uint32_t v = u * 64u + lane < n ? 1u : 0u;
+    const uint32_t o = v ? min(o_raw, dlen) : 0u;
+    const uint32_t l = v ? min(c_raw, dlen - o) : 0u;
+    off = o;  // a packet reaching past data_len is clamped to the buffer
+    end = o + l;
+    return v;
+  };
+  auto fb_append = [&](uint32_t i, uint32_t fb) {  // the tile's leftovers go to the fallback list
+    const uint64_t m = __ballot(fb != 0);
+    if (m) {
+      if (fb) P.fb_list[fb_start + fb_c + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = i;
+      fb_c += (uint32_t)__popcll(m);
+    }
+  };
+  // A tile's byte run [t0, t0 + 8192 nr): its packets' extent, in nr rounds; nr = 0 when the
+  // packets are not nearly back to back (or hold no bytes): the tile goes to the fallback list.
+  uint32_t t0_p = 0, t1_p = 0, nr_p = 0;
+  auto tile_plan = [&](uint32_t valid, uint32_t off, uint32_t end) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(wave_min(valid ? (off & ~15u) : 0xFFFFFFFFu));
+    const uint32_t hi = __builtin_amdgcn_readfirstlane(wave_max(valid ? end : 0u));
+    const uint32_t bytes = __builtin_amdgcn_readfirstlane(wave_sum(valid ? min(end - off, 1u << 24) : 0u));
+    t0_p = lo;
+    t1_p = hi;
+    nr_p = (hi > lo && (uint64_t)(hi - lo) <= 2ull * bytes + kRoStage) ? (hi - lo + kRoStage - 1u) / kRoStage : 0u;
+  };
+  v4u32 wv[NC];
+  auto rload = [&](uint32_t base, uint32_t nbytes) {  // one round's bytes into the registers
+#pragma unroll
+    for (int j = 0; j < NC; j++) {
+      const uint32_t c = 1024u * j + 16u * lane;
+      wv[j] = __builtin_nontemporal_load(reinterpret_cast<const v4u32 *>(P.data + base + (c < nbytes ? c : 0u)));
+    }
+    __builtin_amdgcn_sched_barrier(0);  // issue them here, ahead of the decode
+  };
+
+  // prologue: the first tile that has rounds (tiles without go to the fallback list whole)
+  uint32_t o_a, c_a, o_b, c_b, off_p, end_p, valid_p;
+  {
+    uint32_t o0, c0;
+    dload(tp, o0, c0);
+    dload(tp + nwaves, o_a, c_a);
+    dload(tp + 2u * nwaves, o_b, c_b);
+    valid_p = dread(tp, o0, c0, off_p, end_p);
+  }
+  tile_plan(valid_p, off_p, end_p);
+  bool any = true;
+  while (nr_p == 0u) {
+    fb_append(tp * 64u + lane, valid_p);
+    if (tp + nwaves >= ntiles) { any = false; break; }
+    tp += nwaves;
+    valid_p = dread(tp, o_a, c_a, off_p, end_p);
+    o_a = o_b;
+    c_a = c_b;
+    dload(tp + 2u * nwaves, o_b, c_b);
+    tile_plan(valid_p, off_p, end_p);
+  }
+  if (any) {
+    uint32_t rp = 0;  // the planner's round of tile tp
+    rload(t0_p, min(kRoStage, ((t1_p - t0_p) + 15u) & ~15u));
+    // decode state: round rd of tile td (its run from t0_d, nr_d rounds)
+    uint32_t td = tp, t0_d = t0_p, nr_d = nr_p, rd = 0;
+    uint32_t off_d = off_p, end_d = end_p;
+    uint32_t base = 0;  // G at the round's start: the sum of the tile's earlier rounds' chunks
+    // per lane, packed (registers bound the waves per SIMD): ls = its header's round (bits 0-15)
+    // | staged | tail pending | odd segment start | fallback | tail bytes (20-23) | valid (24);
+    // tB: the pending tail's B (tile-relative); part: the segment's partial sum
+    constexpr uint32_t kStaged = 1u << 16, kPend = 1u << 17, kOdd = 1u << 18, kFb = 1u << 19, kValid = 1u << 24;
+    uint32_t ls = valid_p ? kValid : 0u, tB = 0, part = 0;
+    Hdr hh;  // (written where the header is staged; read only for a staged lane)
+    for (;;) {
+      // ---- the previous round's last bytes and prefix words in front of this round's
+      if (rd > 0u) {
+        if (lane < 9u) {
+          const v4u32 q = *reinterpret_cast<const v4u32 *>(g_lds + buf + kRoStage - 144u + 16u * lane);
+          const uint32_t pc = lds_u32(pfx + 4u * (503u + lane)) - lds_u32(pfx + 4u * 512u);
+          *reinterpret_cast<v4u32 *>(g_lds + buf - 144u + 16u * lane) = q;
+          *reinterpret_cast<uint32_t *>(g_lds + pfx - 36u + 4u * lane) = pc;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+      // ---- commit round rd: registers -> LDS, and its chunk prefix sums from the registers
+      {
+        uint32_t cs[NC];
+#pragma unroll
+        for (int j = 0; j < NC; j++) {
+          *reinterpret_cast<v4u32 *>(g_lds + buf + 1024u * j + 16u * lane) = wv[j];
+          cs[j] = dot2(wv[j].w, 0x00010001u, dot2(wv[j].z, 0x00010001u,
+                       dot2(wv[j].y, 0x00010001u, dot2(wv[j].x, 0x00010001u, 0u))));
+        }
+        rows_prefix<NC>(cs, pfx, lane);
+      }
+      // ---- plan and load the next round (the rest of this tile, or the next tile with rounds)
+      bool has_next = false, new_tile = false;
+      if (rp + 1u < nr_p) {
+        rp++;
+        has_next = true;
+      } else {
+        while (tp + nwaves < ntiles) {
+          tp += nwaves;
+          valid_p = dread(tp, o_a, c_a, off_p, end_p);
+          o_a = o_b;
+          c_a = c_b;
+          dload(tp + 2u * nwaves, o_b, c_b);
+          tile_plan(valid_p, off_p, end_p);
+          if (nr_p) {
+            rp = 0;
+            has_next = new_tile = true;
+            break;
+          }
+          fb_append(tp * 64u + lane, valid_p);
+        }
+      }
+      if (has_next) {
+        const uint32_t rb = t0_p + kRoStage * rp;
+        rload(rb, min(kRoStage, (t1_p - rb + 15u) & ~15u));
+      }
+      // ---- round rd of tile td
+      const uint32_t R0 = t0_d + kRoStage * rd;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the committed round is readable)
+      if (rd == 0u && (ls & kValid)) {
+        const uint32_t need = max(min(off_d + kRoHdr, end_d), off_d + 1u);
+        ls = kValid | ((need - 1u - t0_d) / kRoStage);
+      }
+      const bool here = (ls & kValid) && (ls & 0xFFFFu) == rd;
+      if (here) {  // stage the header; the segment's head, and its tail if in this round
+        const uint32_t pl = buf + off_d - R0;  // (>= buf - 128: the carry)
+        uint32_t l4 = 0, seg = 0;
+        ls |= kStaged;
+        if (hdr_parse(pl, end_d - off_d, hh, F, vxreg, l4, seg) && CS) {
+          const uint32_t S = pl + l4, E = S + seg, A = (S + 15u) & ~15u, B = E & ~15u;
+          ls |= (S & 1u) ? kOdd : 0u;
+          if (E <= A) {  // the whole segment inside its first chunk
+            part = (A > S) ? chunk_part(A - 16u, S & 15u, E - (A - 16u), 0u) : 0u;
+          } else {
+            part = (A > S) ? chunk_part(A - 16u, S & 15u, 16u, 0u) : 0u;
+            part -= base + lds_u32(pfx + 4u * (uint32_t)((int32_t)(A - buf) >> 4));
+            if (E > B ? B < buf + kRoStage : B <= buf + kRoStage) {
+              part += base + lds_u32(pfx + 4u * ((B - buf) >> 4));
+              if (E > B) part = chunk_part(B, 0u, E - B, part);
+            } else {
+              ls |= kPend | ((E - B) << 20);
+              tB = B - buf + R0 - t0_d;
+            }
+          }
+        }
+        // VXLAN frames (their inner headers are not staged) take the generic decoder: a second
+        // straight-line decode in the loop would cost the kernel its third wave per SIMD
+        if (hh.ok == 2u) ls |= kFb;
+      } else if (ls & kPend) {  // a segment's tail in this round?
+        const uint32_t rel = tB - (R0 - t0_d), tl = (ls >> 20) & 15u;
+        if (tl ? rel < kRoStage : rel <= kRoStage) {
+          part += base + lds_u32(pfx + 4u * (rel >> 4));
+          if (tl) part = chunk_part(buf + rel, 0u, tl, part);
+          ls &= ~kPend;
+        }
+      }
+      base += lds_u32(pfx + 4u * 512u);
+      // ---- the tile is complete after its last round: one decode from the staged headers
+      if (rd + 1u == nr_d) {
+        Out res;
+        uint32_t fb = 0;
+        if ((ls & (kStaged | kPend | kFb)) == kStaged) {
+          // an odd-aligned segment's sum is in the other byte order: folded and swapped back
+          const uint32_t f1 = (part >> 16) + (part & 0xFFFFu), f2 = (f1 >> 16) + (f1 & 0xFFFFu);
+          hh.sum = (ls & kOdd) ? __builtin_amdgcn_perm(0u, f2, 0x0C0C0001u) : part;
+          Seg none{0, 0, 0};
+          if (!fast_decode<CS, HASH, true, true>(0u, end_d - off_d, F, res, buf, none, &hh)) fb = 1;
+        } else {
+          fb = 1;
+        }
+        const uint32_t i = td * 64u + lane;
+        const uint32_t valid = (ls & kValid) ? 1u : 0u;
+        fb_append(i, valid ? fb : 0u);
+        if (valid && !fb) store_out(P, i, res);
+      }
+      if (!has_next) break;
+      if (new_tile) {
+        td = tp;
+        t0_d = t0_p;
+        nr_d = nr_p;
+        rd = 0;
+        off_d = off_p;
+        end_d = end_p;
+        ls = valid_p ? kValid : 0u;
+        base = 0;
+      } else {
+        rd++;
       }
     }
   }
+  if (lane == 0u) P.fb_wcount[gw] = fb_c;  // (gpd_last_launch_split's count)
+  decode_fallback_list<kRoStage / 64u>(P, buf, fb_start, fb_c, lane, dlen, options);
 }
 
 template <int STAGE, bool FAST, bool EXT, bool PAGES, bool SWZ, int WAVES, bool CS = true,
@@ -2140,8 +2455,27 @@ static hipError_t launch_rs(KParams &P, hipStream_t stream, int num_cus) {
 // per SIMD (VGPRs <= 512 / MINW): 4 for 4 KiB windows, 3 for 8 KiB — what LDS admits, no
 // spills.  The register-computed chunk prefix pays off for long frames only (IMIX -3 %); with
 // small frames (pcap records, VXLAN) its extra registers and code cost 1-2 %.
+template <bool CS, bool HASH, int MINW>
+static hipError_t launch_ro(KParams &P, hipStream_t stream, int num_cus) {
+  const uint64_t ntiles = (P.n + 63) / 64;
+  const size_t lds = ((P.image_words * 4u + 15u) & ~15u) + 4 * (size_t)ro_wave_lds_bytes() + 64;
+  const uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>((160u * 1024u) / lds, MINW));
+  uint64_t blocks = (ntiles + 3) / 4;
+  const uint64_t cap = (uint64_t)num_cus * per_cu * kGridRounds;
+  if (blocks > cap) blocks = cap;
+  P.fb_waves = (uint32_t)blocks * 4u;
+  if (blocks == 0) return hipSuccess;
+  if (P.fb_waves > (uint32_t)num_cus * kMaxFastWavesPerCU) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((ro_kernel<CS, HASH, MINW>), dim3((unsigned)blocks), dim3(256), lds, stream, P);
+  return hipGetLastError();
+}
+
 template <bool CS, bool HASH>
 static hipError_t launch_fast(KParams &P, hipStream_t stream, int num_cus) {
+  if (P.options & kRounds) {  // header-once over 8 KiB rounds of each tile's run (ro_kernel)
+    if (P.waves == 2) return launch_ro<CS, HASH, 2>(P, stream, num_cus);
+    return launch_ro<CS, HASH, 3>(P, stream, num_cus);
+  }
   if (P.stage == 4096) {
     if (P.waves == 2) return launch_rs<4096, CS, HASH, 2>(P, stream, num_cus);
     if (P.waves == 3) return launch_rs<4096, CS, HASH, 3>(P, stream, num_cus);
@@ -2342,10 +2676,6 @@ hipError_t launch_ip4_frag(const FragArgs &A, hipStream_t stream, int num_cus) {
   return hipGetLastError();
 }
 
-__global__ __launch_bounds__(256) void noop_kernel(uint32_t *w) {
-  if (w[0] == 0xFFFFFFFFu && threadIdx.x == 1000u) w[1] = 0u;  // (never true: one read, then exit)
-}
-
 bool fast_eligible(const KParams &P) {
   // the fast kernel: Ethernet first and registered, hashed tables, no extended records
   return !P.ext && !P.use_pages && P.fixed && P.first == GPD_LT_ETHERNET &&
@@ -2368,11 +2698,6 @@ hipError_t launch_decode(const KParams &P0, hipStream_t stream, int num_cus, hip
     if (e != hipSuccess) return e;
     if (fb_waves) *fb_waves = P.fb_waves;
     if (mid && (e = hipEventRecord(mid, stream)) != hipSuccess) return e;
-    if (kExp & 16u) {  // A/B: a second, empty launch after the fast kernel (the old list kernel's shape)
-      hipLaunchKernelGGL(noop_kernel, dim3(std::max<unsigned>((unsigned)num_cus * 2, (P.fb_waves + 3u) / 4u)),
-                         dim3(256), 0, stream, P.fb_wcount);
-      return hipGetLastError();
-    }
     return hipSuccess;  // (each fast wave decodes its own fallback list: one launch)
   }
   if (P.ext) return P.use_pages ? launch_s<true, true>(P, stream, num_cus)

@@ -487,9 +487,10 @@ int gpd_ctx_set_tuning(gpd_ctx *ctx, const gpd_tuning *t) {
   if (t->window_bytes != 0 && t->window_bytes != 4096 && t->window_bytes != 8192)
     return set_err(GPD_ERR_INVALID, "gpd_ctx_set_tuning: window_bytes %u (0, 4096 or 8192)", t->window_bytes);
   if (t->shift < -1 || t->shift > 1 || t->reg_prefix < -1 || t->reg_prefix > 1 || t->header_once < -1 ||
-      t->header_once > 1 || t->device_walk < -1 || t->device_walk > 1)
+      t->header_once > 2 || t->device_walk < -1 || t->device_walk > 1)
     return set_err(GPD_ERR_INVALID,
-                   "gpd_ctx_set_tuning: shift / reg_prefix / header_once / device_walk outside {-1, 0, 1}");
+                   "gpd_ctx_set_tuning: shift / reg_prefix / device_walk outside {-1, 0, 1}, header_once "
+                   "outside {-1, 0, 1, 2}");
   if (t->waves_per_simd != 0 && (t->waves_per_simd < 2 || t->waves_per_simd > 4))
     return set_err(GPD_ERR_INVALID, "gpd_ctx_set_tuning: waves_per_simd %d (0, 2, 3 or 4)", t->waves_per_simd);
   ctx->tune = *t;
@@ -595,6 +596,8 @@ static int launch(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, hipS
   if (P.stage == 8192 &&
       (ctx->tune.header_once >= 0 ? ctx->tune.header_once != 0 : (mean_slot > 160 && !shift)))
     P.options |= 1u << 25;
+  // ... over 8 KiB rounds of each tile's contiguous run instead of packet-cut windows
+  if (ctx->tune.header_once == 2) P.options |= 1u << 24;
   P.waves = (uint32_t)ctx->tune.waves_per_simd;
   P.nstores = out->records ? 2u + (out->hdr_off != nullptr)
                            : 2u + (out->net_hash != nullptr) + (out->tp_hash != nullptr) +

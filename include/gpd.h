@@ -371,7 +371,8 @@ int  gpd_sync(gpd_ctx *ctx, void *stream);
 int  gpd_ctx_set_timing(gpd_ctx *ctx, int enable);
 float gpd_last_kernel_ms(gpd_ctx *ctx);
 /* The last timed gpd_decode split in two (synchronises its stream): the packets the fast
- * decode left to the generic decoder (options, fragments, hop-by-hop, errors, ...), the fast
+ * decode left to the generic decoder (IPv4 options, hop-by-hop, LLC, errors, ...; IPv4 fragments
+ * decode on the fast path), the fast
  * kernel's time (each of its waves decodes its own fallback list at its end, so that time
  * includes the generic decodes) and the time after it to the end of the call (ms, ~0).  Needs a
  * timed launch that took the fast path (Ethernet first, hashed tables, no ext records). */
@@ -391,7 +392,9 @@ typedef struct gpd_tuning {
                               (4 KiB windows) or 2, 3 (8 KiB windows) */
   int32_t  header_once;   /* 8 KiB windows: decode each 64-packet tile once from headers staged
                              as its windows pass, instead of once per window: -1 automatic
-                             (mean slot > 160 B), 0 off, 1 on */
+                             (mean slot > 160 B), 0 off, 1 on; 2: the same over 8 KiB rounds of
+                             each tile's contiguous byte run instead of windows cut at packet
+                             boundaries (packets larger than a window stay on the fast path) */
   int32_t  device_walk; /* gpd_decode_pcap(_at): find the records in HBM after the raw
                                bytes arrive (gpd_pcapwalk.hip) instead of walking them on the
                                host first: -1 automatic (on), 0 off, 1 on */

@@ -258,13 +258,15 @@ def test_window_sizes_both_ways(window):
 
 @pytest.mark.parametrize("extra", [{}, {"reg_prefix": 0}, {"shift": 1}, {"waves_per_simd": 2}],
                          ids=["default", "lds_prefix", "shifted", "two_waves"])
-@pytest.mark.parametrize("ho", [0, 1])
+@pytest.mark.parametrize("ho", [0, 1, 2])
 def test_header_once_both_ways(ho, extra):
     """8 KiB windows decode a tile either once per window (the lanes each window holds) or
     once per tile from the headers seg_pass staged in registers as the windows passed, with
-    the transport segment summed in its window (header_once).  Force each, over layouts whose
-    tiles span one window or several, TCP options (mutations), VXLAN (which the header-once
-    decode leaves to the generic decoder) and unaligned / pcap-like offsets."""
+    the transport segment summed in its window (header_once 1), or once per tile over 8 KiB
+    rounds of the tile's contiguous run (header_once 2, ro_kernel: segments summed across
+    rounds).  Force each, over layouts whose tiles span one window or several, TCP options
+    (mutations), VXLAN (which the header-once decode leaves to the generic decoder) and
+    unaligned / pcap-like offsets (odd segment starts)."""
     t = dict(window_bytes=8192, header_once=ho, **extra)
     pk = _golden_packets()
     run_both(PacketBatch.from_packets(pk), ext=False, tuning=t)
@@ -278,11 +280,12 @@ def test_header_once_both_ways(ho, extra):
     run_both(NP.index(cap).batch, ext=False, tuning=t)
 
 
-def test_header_once_tile_shapes():
-    """The header-once kernel over batch shapes that stress its tiles and windows: 1..200
-    packets (fewer tiles than waves, a partial last tile), tiles in reverse and shuffled order,
-    frames larger than a window between small ones, and a long IMIX batch."""
-    t = dict(window_bytes=8192, header_once=1)
+@pytest.mark.parametrize("ho", [1, 2])
+def test_header_once_tile_shapes(ho):
+    """The header-once kernels over batch shapes that stress their tiles and windows / rounds:
+    1..200 packets (fewer tiles than waves, a partial last tile), tiles in reverse and shuffled
+    order, frames larger than a window between small ones, and a long IMIX batch."""
+    t = dict(window_bytes=8192, header_once=ho)
     base = synth.make_imix(1 << 12, seed=0x5EED0401)
     pk = [base.packet(i) for i in range(base.n)]
     for m in (1, 63, 64, 65, 130, 200):
@@ -350,7 +353,7 @@ def _ip4_option_frames(n, seed):
     return out
 
 
-@pytest.mark.parametrize("ho", [0, 1])
+@pytest.mark.parametrize("ho", [0, 1, 2])
 def test_ip4_options_both_ways(ho):
     """IPv4 options on long frames: the header-once kernel walks them in seg_pass (ip4_options)
     and decodes the packets in its straight-line pass; the per-window kernel leaves them to the
@@ -359,6 +362,34 @@ def test_ip4_options_both_ways(ho):
     run_both(PacketBatch.from_packets(_ip4_option_frames(1 << 12, 0x5EED0501)), ext=False, tuning=t)
     pk = _ip4_option_frames(1 << 11, 0x5EED0502)
     run_both(PacketBatch.from_packets(pk, align=1), ext=False, tuning=t)
+
+
+@pytest.mark.parametrize("waves", [2, 3])
+def test_round_kernel_long_segments(waves):
+    """ro_kernel (header_once 2) sums a transport segment across any number of 8 KiB rounds:
+    TCP and UDP frames of 1 B .. 64 KiB between IMIX frames (segments ending on, before and
+    after round and chunk boundaries), at 16-byte and odd offsets (the segment summed in the
+    other byte order), with right and wrong checksums, against the oracle — the jumbo frames on
+    the fast path here, where the windowed kernels hand them to the generic decoder."""
+    import error_sites as ES
+    rng = np.random.default_rng(0x5EED0601)
+    base = synth.make_imix(1 << 11, seed=0x5EED0602)
+    pk = [base.packet(i) for i in range(base.n)]
+    sizes = [0, 1, 15, 16, 17, 1000, 8100, 8175, 8176, 8177, 8192, 8193, 9000, 16370, 16384, 30001,
+             65400]
+    k = 0
+    for sz in sizes:
+        for proto in (6, 17):
+            body = bytes(rng.integers(0, 256, sz, dtype=np.uint8))
+            l4 = ES.tcp(body) if proto == 6 else ES.udp(body)
+            if len(l4) + 20 > 65535:
+                l4 = l4[:65535 - 20]
+            p = ES.eth(0x0800, ES.ip4(l4, proto=proto))
+            pk.insert(31 * k + 7, p)
+            k += 1
+    t = dict(header_once=2, waves_per_simd=waves)
+    for align in (16, 1):
+        run_both(PacketBatch.from_packets(pk, align=align), ext=False, tuning=t)
 
 
 def test_layouts_unaligned_shuffled_large_empty():
@@ -562,7 +593,8 @@ def test_full_size_config4_vxlan_exact():
 @pytest.mark.parametrize("mask", [ALL, 0x3FF])
 def test_traffic_mix_both_kernels(mask):
     """The traffic mix (ICMPv4 echo, 802.3/LLC, IPv6/TCP, VXLAN, TCP/UDP, and the generic
-    decoder's share: IPv4 options, fragments, IPv6 hop-by-hop, cut TCP headers) with every
+    decoder's share: IPv4 options, IPv6 hop-by-hop, cut TCP headers; its IPv4 fragments decode on
+    the fast path) with every
     decoder registered and without ICMPv4/LLC (they then stop as unsupported)."""
     run_both(synth.make_traffic_mix(1 << 15), mask=mask, ext=True)
     run_both(synth.make_traffic_mix(1 << 15, seed=9), mask=mask, options=1, ext=False)
