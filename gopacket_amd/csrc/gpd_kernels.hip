@@ -1073,15 +1073,7 @@ __device__ __forceinline__ void seg_pass(uint32_t p, uint32_t len, uint32_t buf,
 template <bool CS, bool HASH, bool COOP, bool HO = false, bool AL = false>
 __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const FastCtx &F, Out &o,
                                             uint32_t buf, Seg &sg, const Hdr *h = nullptr) {
-  // nh: the last network layer's NetworkFlow().FastHash() — in the two-pass decode, for IPv4 its
-  // two raw address words, hashed once at the end; tpx: the last transport's raw port word,
-  // likewise.  (A VXLAN frame's outer IPv4 and UDP layers are overwritten by its inner pass,
-  // A11: hashing them as they were accepted cost ~70 VALU per packet for nothing.  The one-pass
-  // header-once decode hashes as it accepts: deferred, the hashes' temporaries overlap and cost
-  // it ~30 VGPRs.)
-  constexpr bool DEFER_HASH = false;  // (measured: +20-45 VGPRs and spills at 3-4 waves per SIMD)
   uint64_t codes = 0, nh = 0, th = 0;
-  uint32_t tpx = 0;
   uint32_t nc = 0, trunc = 0, stop = 0;
   uint32_t net = 0, tp = 0, ip4 = 0, ipcs = 0;
   uint32_t tp_off = 0, tp_len = 0, tp_pl = 0;  // the last transport; its proto + length terms
@@ -1178,8 +1170,7 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
                            dot2(W[0], 0x00010001u, ps))));
         ip4 = 1;
       }
-      if (HASH) nh = DEFER_HASH ? ((uint64_t)W[4] << 32) | W[3]  // ip4.go:63-65, hashed at the end
-                                : flow_fast(fnv_start<4>(W[3]), fnv_start<4>(W[4]), 1u);
+      if (HASH) nh = flow_fast(fnv_start<4>(W[3]), fnv_start<4>(W[4]), 1u);  // ip4.go:63-65
       ps4 = ps;
       net = 1;
       net_off = l3;
@@ -1247,8 +1238,7 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
       put(GPD_C_UDP);
     }
     tp = g;
-    tpx = tx;  // tcp.go:331-333 / udp.go:123-125: the ports
-    if (HASH && !DEFER_HASH) th = flow_fast(fnv_start<2>(tx), fnv_start<2>(tx >> 16), g == 1u ? 4u : 5u);
+    if (HASH) th = flow_fast(fnv_start<2>(tx), fnv_start<2>(tx >> 16), g == 1u ? 4u : 5u);
     // pseudo-header protocol and length as LE-domain words (seg < 2^16 in a window); the
     // addresses are added at the end from the network object of this kind as the call
     // leaves it (SetNetworkLayerForChecksum(&ip4) reads the reused object: for VXLAN whose
@@ -1275,10 +1265,6 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
   }
 
   // ---- outputs, composed exactly as decode_packet does
-  if (HASH && DEFER_HASH) {
-    if (net == 1u) nh = flow_fast(fnv_start<4>((uint32_t)nh), fnv_start<4>((uint32_t)(nh >> 32)), 1u);
-    if (tp) th = flow_fast(fnv_start<2>(tpx), fnv_start<2>(tpx >> 16), tp == 1u ? 4u : 5u);
-  }
   const uint32_t tp_ps = tp_pl + (tp_kind == 1u ? ps4 : ps6);
   uint32_t st = (stop ? F.unsup : GPD_ST_OK) | (trunc << 2) | (nc << 4);
   uint32_t cs = 0;

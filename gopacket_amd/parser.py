@@ -251,7 +251,8 @@ class DecodingLayerParser:
 
     # Engine tuning (gpd_ctx_set_tuning): staging choices that never change a result.
     # Keys: window_bytes (0 auto / 4096 / 8192), shift and reg_prefix (-1 auto / 0 / 1),
-    # waves_per_simd (0 auto / 2 / 3 / 4), header_once and device_walk (-1 auto / 0 / 1).
+    # waves_per_simd (0 auto / 2 / 3 / 4), header_once (-1 auto / 0 / 1 windows / 2 rounds) and
+    # device_walk (-1 auto / 0 / 1).
     Tuning: Optional[dict] = None
 
     def _apply_tuning(self):

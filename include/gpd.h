@@ -390,11 +390,11 @@ typedef struct gpd_tuning {
                              -1 automatic (mean slot > 160 B), 0 off, 1 on */
   int32_t  waves_per_simd; /* resident waves of the fast kernel per SIMD: 0 automatic, 2, 3, 4
                               (4 KiB windows) or 2, 3 (8 KiB windows) */
-  int32_t  header_once;   /* 8 KiB windows: decode each 64-packet tile once from headers staged
-                             as its windows pass, instead of once per window: -1 automatic
-                             (mean slot > 160 B), 0 off, 1 on; 2: the same over 8 KiB rounds of
-                             each tile's contiguous byte run instead of windows cut at packet
-                             boundaries (packets larger than a window stay on the fast path) */
+  int32_t  header_once;   /* decode each 64-packet tile once from headers staged as its bytes
+                             pass, instead of once per window: 0 off, 1 over 8 KiB windows cut at
+                             packet boundaries, 2 over 8 KiB rounds of the tile's contiguous byte
+                             run (packets larger than a window stay on the fast path); -1
+                             automatic: 2 when the mean slot exceeds 160 B, else 0 */
   int32_t  device_walk; /* gpd_decode_pcap(_at): find the records in HBM after the raw
                                bytes arrive (gpd_pcapwalk.hip) instead of walking them on the
                                host first: -1 automatic (on), 0 off, 1 on */

@@ -730,13 +730,13 @@ def test_record_form_equals_soa():
     assert rc == GPD_ERR_INVALID
 
 
-@pytest.mark.parametrize("ho", [0, 1])
+@pytest.mark.parametrize("ho", [0, 1, 2])
 def test_long_frame_mutations_both_ways(ho):
     """Long frames (a header-once batch: 8 KiB windows, tiles spanning several) with their
     headers fuzzed — EtherType and tags, IPv4 version/IHL/length/flags/protocol, TCP data
     offset and option bytes (the Timestamps shortcut's pattern among them), UDP length — and
     cut at random lengths, mixed among intact IMIX frames, against the oracle with
-    header-once forced off and on."""
+    header-once forced off, per window and per round."""
     rng = np.random.default_rng(41 + ho)
     base = synth.make_imix(1 << 12)
     n = base.n
