@@ -194,6 +194,13 @@ bool build_fixed(const uint16_t *eth, const uint16_t *tcp, const uint16_t *udp,
 
 }  // namespace
 
+// Staging slots of the host-memory paths (gpd_decode_host and the host-walk pcap path cycle
+// through all of them; the device-walk pcap and TPACKET_V3 paths pair slots 0 and 1).
+#ifndef GPD_EXP
+#define GPD_EXP 0
+#endif
+constexpr int kHostSlots = (GPD_EXP & 2) ? 3 : 2;  // (A/B builds: a third slot)
+
 struct gpd_ctx {
   int device = 0;
   int num_cus = 256;
@@ -243,7 +250,7 @@ struct gpd_ctx {
     uint64_t lo = 0, hi = 0;  // packet range in flight
     bool busy = false;
     bool direct = false;      // its results go straight into the caller's (registered) arrays
-  } slot[2];
+  } slot[kHostSlots];
   uint64_t slot_bytes = 0, slot_pkts = 0;
   gpd::PwCtl *d_pw_ctl = nullptr, *h_pw_ctl = nullptr;  // one control block per slot
   hipEvent_t ev_pw[2] = {nullptr, nullptr};            // a slot's chunk walked (and its block read back)
@@ -945,7 +952,7 @@ int gpd_decode_host(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out) {
     s.hi = j;
     s.busy = true;
     i = j;
-    k ^= 1;
+    k = (k + 1) % kHostSlots;
   }
   for (auto &s : ctx->slot) {
     if (s.busy) {
@@ -1127,7 +1134,7 @@ static int decode_pcap_host_walk(gpd_ctx *ctx, const uint8_t *buf, uint64_t len,
       s.hi = done + j;
       s.busy = true;
       i = j;
-      k ^= 1;
+      k = (k + 1) % kHostSlots;
     }
     done += n;
     *n_out = done;
