@@ -669,6 +669,21 @@ def host_buffer(nbytes: int, shared: bool, local: int, key: str, dist):
     return np.frombuffer(mm, np.uint8), mm, path
 
 
+def bind_local(arr, local: int) -> dict:
+    """Put a host buffer's pages on the GPU's NUMA node before they are written
+    (gpd_host_bind_local): the PCIe-inclusive leg streams the capture from there, not across
+    the socket link (r04: a capture first-touched by the generator's threads lay 44 % on the
+    far node, and the calls that read it ran 1.1-1.7x longer)."""
+    import ctypes as C
+    from gopacket_amd._lib import lib
+    node = C.c_int(-1)
+    rc = lib.gpd_host_bind_local(local, arr.ctypes.data, arr.nbytes, C.byref(node))
+    out = {"node": node.value, "rc": rc}
+    if rc:
+        out["error"] = lib.gpd_last_error_string().decode()
+    return out
+
+
 PCAP_FILE_HEADER = (0xA1B2C3D4, 2, 4, 0, 0, 262144, 1)  # pcapgo framing: LE, microseconds
 
 
@@ -690,7 +705,7 @@ class ReplayCapture:
     `cap` is the rank's buffer, [start, end) its shard's records in it."""
 
     def __init__(self, args, n: int, world: int, rank: int, local: int, dist, threads: int,
-                 bcast_device):
+                 bcast_device, gpu=None):
         import struct
         from gopacket_amd import pcap as NP
         from gopacket_amd import synth
@@ -703,6 +718,7 @@ class ReplayCapture:
         if self.mode == "private":
             m = hi - lo
             cap, mm, _ = host_buffer(24 + 80 * m + PAD, False, local, key, dist)
+            self.bind = bind_local(cap, gpu) if args.numa_bind and gpu is not None else None
             cap[:24] = hdr
             synth.udp64_native(cap[24:24 + 80 * m], lo, hi, REPLAY_SEED, records=True, nthreads=threads)
             cap[24 + 80 * m:] = 0
@@ -713,6 +729,9 @@ class ReplayCapture:
                 dist.barrier()
             return
         cap, mm, path = host_buffer(24 + 80 * n + PAD, True, local, key, dist)
+        # this rank's records on its GPU's node (each rank writes and streams only its own)
+        self.bind = (bind_local(cap[24 + 80 * lo:24 + 80 * hi], gpu) if args.numa_bind and gpu is not None
+                     else None)
         try:
             if rank == 0:
                 cap[:24] = hdr
@@ -807,7 +826,7 @@ def bench_replay(args, world, rank, local, dist):
     dev = torch.device("cuda", local)
     t0 = time.perf_counter()
     host_local = int(os.environ.get("LOCAL_RANK", local))  # the host roles (--same-device keeps them)
-    rc = ReplayCapture(args, n, world, rank, host_local, dist, threads, COMM_DEVICE or dev)
+    rc = ReplayCapture(args, n, world, rank, host_local, dist, threads, COMM_DEVICE or dev, gpu=local)
     cap, mm = rc.cap, rc.mm
     t_gen = time.perf_counter() - t0
     dl = rc.data_len
@@ -912,7 +931,7 @@ def bench_replay(args, world, rank, local, dist):
         dist.barrier()
     # where the time of the PCIe-inclusive leg goes: each call's wall time and its phases
     # (gpd_decode_pcap_last_times: walk, staging, waits for the slots' transfers + decode, drain)
-    call_ms, phases = [], np.zeros(6, np.float64)
+    call_ms, phases, call_ph = [], np.zeros(6, np.float64), []
     ph = np.zeros(6, np.float64)
     t0 = time.perf_counter()
     p, done, last = start, 0, 0
@@ -923,6 +942,7 @@ def bench_replay(args, world, rank, local, dist):
         call_ms.append((time.perf_counter() - tc) * 1e3)
         lib.gpd_decode_pcap_last_times(ph.ctypes.data)
         phases += ph
+        call_ph.append(ph.copy())
         assert err is None and k > 0, err
         done += k
         last = k
@@ -936,7 +956,15 @@ def bench_replay(args, world, rank, local, dist):
                  "call_ms_by_quarter": [round(float(q.mean()), 3) for q in np.array_split(cm, 4) if len(q)],
                  "phases_ms_total": dict(zip(["total", "walk", "walk_wait", "stage", "sync", "drain"],
                                              [round(float(x), 1) for x in phases])),
-                 "capture_placement": host_placement(cap, local)}
+                 "capture_placement": host_placement(cap, local), "numa_bind": rc.bind}
+    names = ["total", "walk", "walk_wait", "stage", "sync", "drain"]
+    pcie_diag["slowest_calls"] = [
+        {"call": int(j), "ms": round(float(cm[j]), 2),
+         **{k: round(float(v), 2) for k, v in zip(names, call_ph[j])}}
+        for j in np.argsort(cm)[::-1][:6]]
+    pcie_diag["phases_ms_by_quarter"] = [
+        {k: round(float(v), 1) for k, v in zip(names, np.sum(q, axis=0))}
+        for q in np.array_split(np.array(call_ph), 4) if len(q)]
     # the streamed results of the last call equal the resident ones for the same records
     tail = res.fields(m - last, m)
     same = all(np.array_equal(getattr(out, f)[:last], tail[f])
@@ -1071,6 +1099,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pcie-call-records", type=int, default=0,
                     help="config 5 PCIe-inclusive leg: records per gpd_decode_pcap_at call (default 2^24)")
+    ap.add_argument("--no-numa-bind", dest="numa_bind", action="store_false",
+                    help="config 5: leave the capture's pages where first touch puts them instead of "
+                    "on the GPU's NUMA node (gpd_host_bind_local)")
     ap.add_argument("--no-side", action="store_true", help="skip the other configurations' "
                     "figures (tcp64, imix, vxlan, pcap64) the default udp64 line carries")
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU-baseline timing "

@@ -81,6 +81,7 @@ EXPORTS = {
     "gpd_decode_pcap_last_times": (None, [C.c_void_p]),
     "gpd_host_register": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
     "gpd_host_unregister": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "gpd_host_bind_local": (C.c_int, [C.c_int, C.c_void_p, C.c_uint64, C.POINTER(C.c_int)]),
     # include/gpd_flow.h
     "gpd_flow_create": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.c_void_p)]),
     "gpd_flow_reset": (C.c_int, [C.c_void_p, C.c_void_p]),

@@ -12,8 +12,11 @@
 // One lane per packet.  The decoder already left, per packet, the EndpointTypes of both
 // flows (status bits 20-27) and where their layers sit (hdr_off), so the key is gathered
 // straight from the packet bytes in HBM: 16+16 address bytes, 4 port bytes, the types.
-// Records live in an open-addressing table of 2^k 80-byte records.  A record is claimed by
-// one 64-bit compare-and-swap of the key's fingerprint; the claimer then stores the key.
+// Records live in an open-addressing table of 2^k slots, each split in two: a 64-byte hot
+// record on a line of its own (fingerprint, key, packed counter word, last) — everything a
+// packet of an existing flow reads or updates — and a 16-byte cold record (first, counter
+// spills).  A record is claimed by one 64-bit compare-and-swap of the key's fingerprint; the
+// claimer then stores the key.
 // The per-flow counters are device atomics, folded first over runs of neighbouring lanes on
 // one record (fold_run).  A second launch compares every packet's key with its record's
 // stored key (visible after the launch boundary), so a fingerprint collision is caught and
@@ -38,6 +41,26 @@ constexpr int kFlowThreads = 256;
 static_assert(sizeof(gpd_flow_rec) == 80, "gpd_flow_rec layout (include/gpd_flow.h)");
 
 enum : uint32_t { FS_FLOWS = 0, FS_PACKETS, FS_NOKEY, FS_FULL, FS_COLL, FS_EXPORT, FS_WORDS = 8 };
+// The stats words lie 128 B apart: every wave adds its tallies when it ends, and device-scope
+// atomics on one line serialise at the memory side (~12 ns each), the words of a line together.
+constexpr uint32_t kStatStride = 16;
+__host__ __device__ constexpr uint32_t stat_at(uint32_t w) { return w * kStatStride; }
+
+// A slot of the table, as two records (gpd_flow_export assembles the public gpd_flow_rec).
+// The hot record is one 64-byte line: a packet of a flow that already exists reads its
+// fingerprint and key and updates `cnt` and `last` there, and touches no other line when its
+// sequence number is above every earlier call's (then `first` cannot fall: FlowParams::seen).
+struct alignas(64) FlowHot {
+  uint64_t fp;       // fingerprint | epoch << 56; 0 = empty
+  uint32_t key[10];  // src[16], dst[16], ports, types (flow_key's words)
+  uint64_t cnt;      // packed counter word: packets << B | bytes mod 2^B (add_run)
+  uint64_t last;
+};
+struct FlowCold {
+  uint64_t first;
+  uint64_t spill;  // (byte-field carries) << 32 + (packet-field wraps), see add_run
+};
+static_assert(sizeof(FlowHot) == 64 && sizeof(FlowCold) == 16, "flow table slot layout");
 
 static_assert(sizeof(gpd_flow_key) == 64, "gpd_flow_key layout (include/gpd_flow.h)");
 
@@ -61,7 +84,7 @@ struct FlowParams {
   const uint32_t *offset, *caplen, *status, *hdr_off;
   uint32_t *flow_id;
   uint64_t n, base;
-  gpd_flow_rec *tab;
+  FlowHot *tab;
   uint64_t mask;  // capacity - 1
   unsigned long long *stats;
   // sharding (gpd_flow_keys / gpd_flow_insert_keys)
@@ -77,6 +100,11 @@ struct FlowParams {
   uint32_t cbits = kCountBits;  // gpd_flow_test_counter_bits (kCountBits in production)
   const gpd_record *rec = nullptr;  // results in the gpd_record form (status and hashes there)
   uint64_t tag = 1ull << 56;    // this launch's epoch (1..255) in the fingerprint word's top byte
+  FlowCold *cold = nullptr;     // the slots' cold records, beside tab
+  // 1 + the highest sequence number of every earlier insert call into this table (the host's
+  // count of index_base + n); ~0 when unknown (key records inserted: their sequence numbers
+  // are the senders')
+  uint64_t seen = ~0ull;
 };
 
 // The key of packet i as 10 words: src[16], dst[16], ports (raw wire bytes), types.  Returns
@@ -172,12 +200,13 @@ __device__ __forceinline__ bool fold_run(bool counted, uint64_t s, uint64_t &mn,
 // its totals plainly; every other run adds them with atomics in the verify launch, after
 // those stores (the launch boundary orders them).  So a new flow costs its claim CAS and
 // plain stores, and the atomics are left to packets of flows that already existed.
-__device__ __forceinline__ void store_run(gpd_flow_rec &r, uint64_t mn, uint64_t mx, uint64_t pb, uint32_t B) {
+__device__ __forceinline__ void store_run(FlowHot &r, FlowCold &c, uint64_t mn, uint64_t mx, uint64_t pb,
+                                          uint32_t B) {
   const uint64_t pk = pb >> kPktShift, by = pb & ((1ull << kPktShift) - 1ull);
-  r.first = mn;
   r.last = mx;
-  r.bytes = (pk << B) | (by & ((1ull << B) - 1ull));  // (pk <= 64 < 2^(64-B))
-  r.packets = (by >> B) << 32;
+  r.cnt = (pk << B) | (by & ((1ull << B) - 1ull));  // (pk <= 64 < 2^(64-B))
+  c.first = mn;
+  c.spill = (by >> B) << 32;
 }
 // The packed add.  x = pk << B + by goes in with one atomicAdd that returns the old word; the
 // lane whose add carried out of the byte field (c carries: ((old mod 2^B) + by) >> B) takes
@@ -187,15 +216,20 @@ __device__ __forceinline__ void store_run(gpd_flow_rec &r, uint64_t mn, uint64_t
 //   packets = (word >> B) + wraps << (64-B),   bytes = (word mod 2^B) + carries << B
 // exactly, in any order of the adds.  Carries need 2^40 bytes and wraps 2^24 packets of one
 // flow in production, so the spill atomics are rare; the add's return is the price.
-__device__ __forceinline__ void add_run(gpd_flow_rec &r, uint64_t mn, uint64_t mx, uint64_t pb, uint32_t B) {
+// `later`: mn is above every sequence number of earlier calls (seen) and the record was
+// claimed by one of them, so its `first` is below mn and the cold record is not touched.
+__device__ __forceinline__ void add_run(FlowHot &r, FlowCold &cr, uint64_t mn, uint64_t mx, uint64_t pb,
+                                        uint32_t B, bool later) {
   // `first` only falls: a read at or below mn (a flow seen in an earlier batch) proves the
   // min a no-op; a stale read is only ever larger, and then the atomic runs
-  const uint64_t f = *reinterpret_cast<volatile uint64_t *>(&r.first);
-  if (mn < f) atomicMin(reinterpret_cast<unsigned long long *>(&r.first), (unsigned long long)mn);
+  if (!later) {
+    const uint64_t f = *reinterpret_cast<volatile uint64_t *>(&cr.first);
+    if (mn < f) atomicMin(reinterpret_cast<unsigned long long *>(&cr.first), (unsigned long long)mn);
+  }
   atomicMax(reinterpret_cast<unsigned long long *>(&r.last), (unsigned long long)mx);
   const uint64_t pk = pb >> kPktShift, by = pb & ((1ull << kPktShift) - 1ull), M = (1ull << B) - 1ull;
   const uint64_t x = (pk << B) + by;
-  auto *w = reinterpret_cast<unsigned long long *>(&r.bytes);
+  auto *w = reinterpret_cast<unsigned long long *>(&r.cnt);
   const uint64_t old = atomicAdd(w, (unsigned long long)x);
   const uint64_t c = ((old & M) + by) >> B;
   uint64_t spill = (c << 32) + (old + x < old ? 1ull : 0ull);
@@ -204,20 +238,14 @@ __device__ __forceinline__ void add_run(gpd_flow_rec &r, uint64_t mn, uint64_t m
     const uint64_t old2 = atomicAdd(w, (unsigned long long)(0ull - back));
     if (old2 < back) spill -= 1ull;
   }
-  if (spill) atomicAdd(reinterpret_cast<unsigned long long *>(&r.packets), (unsigned long long)spill);
-}
-__host__ __device__ inline void unpack_counts(gpd_flow_rec &r, uint32_t B) {
-  const uint64_t w = r.bytes, sp = r.packets;
-  r.packets = (w >> B) + ((sp & 0xFFFFFFFFull) << (64u - B));
-  r.bytes = (w & ((1ull << B) - 1ull)) + ((sp >> 32) << B);
+  if (spill) atomicAdd(reinterpret_cast<unsigned long long *>(&cr.spill), (unsigned long long)spill);
 }
 
 // Is the record's stored key the packet's key?
-__device__ __forceinline__ bool same_key(const gpd_flow_rec &r, const uint32_t (&k)[10]) {
-  const uint32_t *w = reinterpret_cast<const uint32_t *>(r.src);
-  bool same = k[9] == ((uint32_t)r.net_type | ((uint32_t)r.tp_type << 8) | ((uint32_t)r.addr_len << 16));
+__device__ __forceinline__ bool same_key(const FlowHot &r, const uint32_t (&k)[10]) {
+  bool same = true;
 #pragma unroll
-  for (int j = 0; j < 9; j++) same = same && w[j] == k[j];
+  for (int j = 0; j < 10; j++) same = same && r.key[j] == k[j];
   return same;
 }
 
@@ -283,13 +311,9 @@ __global__ __launch_bounds__(kFlowThreads) void flow_insert_kernel(FlowParams P)
           old = atomicCAS(reinterpret_cast<unsigned long long *>(&P.tab[s].fp), 0ull,
                           (unsigned long long)(fp | P.tag));
         if (old == 0ull) {  // claimed: store the key (read by the verify launch)
-          gpd_flow_rec &r = P.tab[s];
-          uint32_t *w = reinterpret_cast<uint32_t *>(r.src);
+          FlowHot &r = P.tab[s];
 #pragma unroll
-          for (int j = 0; j < 9; j++) w[j] = k[j];  // src, dst, ports
-          r.net_type = (uint8_t)(k[9] & 0xFFu);
-          r.tp_type = (uint8_t)((k[9] >> 8) & 0xFFu);
-          r.addr_len = (uint8_t)(k[9] >> 16);
+          for (int j = 0; j < 10; j++) r.key[j] = k[j];
           created = true;
           break;
         }
@@ -321,8 +345,8 @@ __global__ __launch_bounds__(kFlowThreads) void flow_insert_kernel(FlowParams P)
     uint32_t start;
     const bool tail = fold_run(counted, s, mn, mx, pb, start);
     if (counted && tail) {
-      if ((made >> start) & 1ull) store_run(P.tab[s], mn, mx, pb, P.cbits);
-      else if (pre) add_run(P.tab[s], mn, mx, pb, P.cbits);
+      if ((made >> start) & 1ull) store_run(P.tab[s], P.cold[s], mn, mx, pb, P.cbits);
+      else if (pre) add_run(P.tab[s], P.cold[s], mn, mx, pb, P.cbits, mn >= P.seen);
     }
     bool bad = false;
     if (counted && pre) bad = !same_key(P.tab[s], k);
@@ -334,11 +358,11 @@ __global__ __launch_bounds__(kFlowThreads) void flow_insert_kernel(FlowParams P)
     wave_tally(t_nokey, live && !keyed);
     wave_tally(t_full, full);
   }
-  wave_flush(P.stats + FS_FLOWS, t_flows);
-  wave_flush(P.stats + FS_PACKETS, t_packets);
-  wave_flush(P.stats + FS_NOKEY, t_nokey);
-  wave_flush(P.stats + FS_FULL, t_full);
-  wave_flush(P.stats + FS_COLL, t_coll);
+  wave_flush(P.stats + stat_at(FS_FLOWS), t_flows);
+  wave_flush(P.stats + stat_at(FS_PACKETS), t_packets);
+  wave_flush(P.stats + stat_at(FS_NOKEY), t_nokey);
+  wave_flush(P.stats + stat_at(FS_FULL), t_full);
+  wave_flush(P.stats + stat_at(FS_COLL), t_coll);
 }
 
 // Second pass: the counter updates of runs that found an existing record, and every item's
@@ -362,7 +386,7 @@ __global__ __launch_bounds__(kFlowThreads) void flow_verify_kernel(FlowParams P)
       pb = (1ull << kPktShift) | caplen;
     }
     const bool tail = fold_run(counted, id, mn, mx, pb, start);
-    if (counted && tail && !((made >> start) & 1ull)) add_run(P.tab[id], mn, mx, pb, P.cbits);
+    if (counted && tail && !((made >> start) & 1ull)) add_run(P.tab[id], P.cold[id], mn, mx, pb, P.cbits, false);
     if (i < P.n) {
       uint32_t k[10];
       uint64_t seq;
@@ -377,7 +401,7 @@ __global__ __launch_bounds__(kFlowThreads) void flow_verify_kernel(FlowParams P)
     }
     wave_tally(t_coll, bad);
   }
-  wave_flush(P.stats + FS_COLL, t_coll);
+  wave_flush(P.stats + stat_at(FS_COLL), t_coll);
 }
 
 // Owner rank of a keyed packet: the high half of the two direction-symmetric FastHashes'
@@ -509,27 +533,39 @@ __global__ __launch_bounds__(kFlowThreads) void flow_ids_scatter_kernel(const gp
   }
 }
 
-__global__ __launch_bounds__(kFlowThreads) void flow_reset_kernel(gpd_flow_rec *tab, uint64_t cap) {
+__global__ __launch_bounds__(kFlowThreads) void flow_reset_kernel(FlowHot *tab, FlowCold *cold, uint64_t cap) {
   for (uint64_t s = blockIdx.x * (uint64_t)kFlowThreads + threadIdx.x; s < cap;
        s += (uint64_t)gridDim.x * kFlowThreads) {
-    gpd_flow_rec r{};
-    r.first = ~0ull;
-    tab[s] = r;
+    tab[s] = FlowHot{};
+    cold[s] = FlowCold{~0ull, 0ull};
   }
 }
 
-__global__ __launch_bounds__(kFlowThreads) void flow_export_kernel(const gpd_flow_rec *tab, uint64_t cap,
-                                                                  gpd_flow_rec *out, uint32_t *idx,
-                                                                  uint64_t max,
+// A slot's two records as the public gpd_flow_rec, counters unpacked:
+//   packets = (cnt >> B) + wraps << (64-B),   bytes = (cnt mod 2^B) + carries << B
+__global__ __launch_bounds__(kFlowThreads) void flow_export_kernel(const FlowHot *tab, const FlowCold *cold,
+                                                                  uint64_t cap, gpd_flow_rec *out,
+                                                                  uint32_t *idx, uint64_t max,
                                                                   unsigned long long *stats, uint32_t B) {
   for (uint64_t s = blockIdx.x * (uint64_t)kFlowThreads + threadIdx.x; s < cap;
        s += (uint64_t)gridDim.x * kFlowThreads) {
-    if (tab[s].fp != 0) {
-      const unsigned long long j = atomicAdd(stats + FS_EXPORT, 1ull);
+    const FlowHot h = tab[s];
+    if (h.fp != 0) {
+      const unsigned long long j = atomicAdd(stats + stat_at(FS_EXPORT), 1ull);
       if (j < max) {
-        gpd_flow_rec r = tab[s];
-        r.fp &= kFpBits;  // the fingerprint without its epoch
-        unpack_counts(r, B);
+        const FlowCold c = cold[s];
+        gpd_flow_rec r{};
+        r.fp = h.fp & kFpBits;  // the fingerprint without its epoch
+        uint32_t *w = reinterpret_cast<uint32_t *>(r.src);
+#pragma unroll
+        for (int k = 0; k < 9; k++) w[k] = h.key[k];  // src, dst, ports
+        r.net_type = (uint8_t)(h.key[9] & 0xFFu);
+        r.tp_type = (uint8_t)((h.key[9] >> 8) & 0xFFu);
+        r.addr_len = (uint8_t)(h.key[9] >> 16);
+        r.first = c.first;
+        r.last = h.last;
+        r.packets = (h.cnt >> B) + ((c.spill & 0xFFFFFFFFull) << (64u - B));
+        r.bytes = (h.cnt & ((1ull << B) - 1ull)) + ((c.spill >> 32) << B);
         out[j] = r;
         idx[j] = (uint32_t)s;
       }
@@ -542,7 +578,8 @@ __global__ __launch_bounds__(kFlowThreads) void flow_export_kernel(const gpd_flo
 struct gpd_flowtable {
   int device = 0;
   int num_cus = 256;
-  gpd_flow_rec *tab = nullptr;
+  gpd::FlowHot *tab = nullptr;   // hot records, 64 B each
+  gpd::FlowCold *cold = nullptr;  // cold records, 16 B each
   uint64_t cap = 0;
   unsigned long long *stats = nullptr;  // FS_WORDS counters
   unsigned long long *parts = nullptr;  // gpd_flow_keys: nparts x grid counts (+ totals), grown on use
@@ -552,6 +589,8 @@ struct gpd_flowtable {
   uint64_t fp_mask = gpd::kFpBits;  // gpd_flow_test_fingerprint_bits
   uint32_t cbits = gpd::kCountBits;  // gpd_flow_test_counter_bits
   uint32_t epoch = 0;                 // insert launches so far, mod 255
+  uint64_t seen = 0;                  // FlowParams::seen, while seen_known
+  bool seen_known = true;             // false after key records went in (until a reset)
 };
 
 // The next insert launch's epoch tag (1..255 in the fingerprint word's top byte).
@@ -601,8 +640,9 @@ int gpd_flow_create(gpd_ctx *ctx, uint64_t capacity, gpd_flowtable **out) {
   ft->num_cus = gpd::ctx_num_cus(ctx);
   ft->cap = cap;
   hipError_t e = hipSetDevice(ft->device);
-  if (e == hipSuccess) e = hipMalloc(&ft->tab, cap * sizeof(gpd_flow_rec));
-  if (e == hipSuccess) e = hipMalloc(&ft->stats, gpd::FS_WORDS * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMalloc(&ft->tab, cap * sizeof(gpd::FlowHot));
+  if (e == hipSuccess) e = hipMalloc(&ft->cold, cap * sizeof(gpd::FlowCold));
+  if (e == hipSuccess) e = hipMalloc(&ft->stats, gpd::stat_at(gpd::FS_WORDS) * sizeof(unsigned long long));
   if (e != hipSuccess) {
     gpd_flow_destroy(ft);
     return gpd::set_error(e == hipErrorOutOfMemory ? GPD_ERR_NOMEM : GPD_ERR_HIP,
@@ -623,9 +663,11 @@ int gpd_flow_reset(gpd_flowtable *ft, void *stream) {
   FLOW_TRY(hipSetDevice(ft->device));
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(gpd::flow_reset_kernel, dim3(grid_for(ft->cap, ft->num_cus)),
-                     dim3(gpd::kFlowThreads), 0, s, ft->tab, ft->cap);
+                     dim3(gpd::kFlowThreads), 0, s, ft->tab, ft->cold, ft->cap);
   FLOW_TRY(hipGetLastError());
-  FLOW_TRY(hipMemsetAsync(ft->stats, 0, gpd::FS_WORDS * sizeof(unsigned long long), s));
+  FLOW_TRY(hipMemsetAsync(ft->stats, 0, gpd::stat_at(gpd::FS_WORDS) * sizeof(unsigned long long), s));
+  ft->seen = 0;
+  ft->seen_known = true;
   return GPD_OK;
 }
 
@@ -648,6 +690,10 @@ int gpd_flow_insert(gpd_flowtable *ft, const gpd_batch *in, const gpd_result *re
   P.rec = res->records;
   P.cbits = ft->cbits;
   P.tag = next_tag(ft);
+  P.cold = ft->cold;
+  P.seen = ft->seen_known ? ft->seen : ~0ull;
+  const uint64_t top = index_base + in->n < index_base ? ~0ull : index_base + in->n;  // (saturating)
+  ft->seen = std::max(ft->seen, top);
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid(grid_for(in->n, ft->num_cus)), block(gpd::kFlowThreads);
   hipLaunchKernelGGL(gpd::flow_insert_kernel<false>, grid, block, 0, s, P);
@@ -732,6 +778,8 @@ int gpd_flow_insert_keys(gpd_flowtable *ft, const gpd_flow_key *keys, uint64_t n
   P.fp_mask = ft->fp_mask;  // (key records carry their sender's fingerprint; recomputed here)
   P.cbits = ft->cbits;
   P.tag = next_tag(ft);
+  P.cold = ft->cold;
+  ft->seen_known = false;  // (P.seen stays ~0: the key records' sequence numbers are unknown here)
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid(grid_for(n, ft->num_cus)), block(gpd::kFlowThreads);
   hipLaunchKernelGGL(gpd::flow_insert_kernel<true>, grid, block, 0, s, P);
@@ -744,9 +792,10 @@ int gpd_flow_insert_keys(gpd_flowtable *ft, const gpd_flow_key *keys, uint64_t n
 int gpd_flow_stats_get(gpd_flowtable *ft, gpd_flow_stats *out, void *stream) {
   if (!ft || !out) return gpd::set_error(GPD_ERR_INVALID, "gpd_flow_stats_get: null argument");
   FLOW_TRY(hipSetDevice(ft->device));
-  unsigned long long h[gpd::FS_WORDS];
-  FLOW_TRY(hipMemcpyAsync(h, ft->stats, sizeof h, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  unsigned long long hs[gpd::stat_at(gpd::FS_WORDS)], h[gpd::FS_WORDS];
+  FLOW_TRY(hipMemcpyAsync(hs, ft->stats, sizeof hs, hipMemcpyDeviceToHost, (hipStream_t)stream));
   FLOW_TRY(hipStreamSynchronize((hipStream_t)stream));
+  for (uint32_t w = 0; w < gpd::FS_WORDS; w++) h[w] = hs[gpd::stat_at(w)];
   out->flows = h[gpd::FS_FLOWS];
   out->packets = h[gpd::FS_PACKETS];
   out->no_key = h[gpd::FS_NOKEY];
@@ -771,10 +820,11 @@ int gpd_flow_export(gpd_flowtable *ft, gpd_flow_rec *out, uint32_t *rec_index, u
   uint32_t *d_idx = nullptr;
   FLOW_TRY(hipMalloc(&d_out, m * sizeof(gpd_flow_rec)));
   hipError_t e = hipMalloc(&d_idx, m * sizeof(uint32_t));
-  if (e == hipSuccess) e = hipMemsetAsync(ft->stats + gpd::FS_EXPORT, 0, sizeof(unsigned long long), s);
+  if (e == hipSuccess) e = hipMemsetAsync(ft->stats + gpd::stat_at(gpd::FS_EXPORT), 0, sizeof(unsigned long long), s);
   if (e == hipSuccess) {
     hipLaunchKernelGGL(gpd::flow_export_kernel, dim3(grid_for(ft->cap, ft->num_cus)),
-                       dim3(gpd::kFlowThreads), 0, s, ft->tab, ft->cap, d_out, d_idx, m, ft->stats, ft->cbits);
+                       dim3(gpd::kFlowThreads), 0, s, ft->tab, ft->cold, ft->cap, d_out, d_idx, m, ft->stats,
+                       ft->cbits);
     e = hipGetLastError();
   }
   std::vector<gpd_flow_rec> recs(m);
@@ -816,6 +866,7 @@ int gpd_flow_destroy(gpd_flowtable *ft) {
   if (!ft) return GPD_OK;
   (void)hipSetDevice(ft->device);
   if (ft->tab) (void)hipFree(ft->tab);
+  if (ft->cold) (void)hipFree(ft->cold);
   if (ft->stats) (void)hipFree(ft->stats);
   if (ft->parts) (void)hipFree(ft->parts);
   if (ft->made) (void)hipFree(ft->made);

@@ -2344,7 +2344,10 @@ __global__ __launch_bounds__(256, MINW) void ro_kernel(KParams P) {
             part = (A > S) ? chunk_part(A - 16u, S & 15u, 16u, 0u) : 0u;
             part -= base + lds_u32(pfx + 4u * (uint32_t)((int32_t)(A - buf) >> 4));
             if (E > B ? B < buf + kRoStage : B <= buf + kRoStage) {
-              part += base + lds_u32(pfx + 4u * ((B - buf) >> 4));
+              // (B may lie in the carry, in front of buf: a frame whose header round is set by
+              // its 128 header bytes while its segment ends before the round, e.g. a short IP
+              // packet in a long frame)
+              part += base + lds_u32(pfx + 4u * (uint32_t)((int32_t)(B - buf) >> 4));
               if (E > B) part = chunk_part(B, 0u, E - B, part);
             } else {
               ls |= kPend | ((E - B) << 20);

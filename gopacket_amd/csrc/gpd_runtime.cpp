@@ -7,12 +7,15 @@
 // options (parser.go:182-195, 336-350), HIP timing events, and the pinned
 // staging used by gpd_decode_host.
 #include <hip/hip_runtime.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <cerrno>
 #include <cstring>
 #include <map>
 #include <string>
@@ -194,13 +197,6 @@ bool build_fixed(const uint16_t *eth, const uint16_t *tcp, const uint16_t *udp,
 
 }  // namespace
 
-// Staging slots of the host-memory paths (gpd_decode_host and the host-walk pcap path cycle
-// through all of them; the device-walk pcap and TPACKET_V3 paths pair slots 0 and 1).
-#ifndef GPD_EXP
-#define GPD_EXP 0
-#endif
-constexpr int kHostSlots = (GPD_EXP & 2) ? 3 : 2;  // (A/B builds: a third slot)
-
 struct gpd_ctx {
   int device = 0;
   int num_cus = 256;
@@ -250,7 +246,7 @@ struct gpd_ctx {
     uint64_t lo = 0, hi = 0;  // packet range in flight
     bool busy = false;
     bool direct = false;      // its results go straight into the caller's (registered) arrays
-  } slot[kHostSlots];
+  } slot[2];  // (a third slot measured 6-9 % slower on config 2's host path, r04)
   uint64_t slot_bytes = 0, slot_pkts = 0;
   gpd::PwCtl *d_pw_ctl = nullptr, *h_pw_ctl = nullptr;  // one control block per slot
   hipEvent_t ev_pw[2] = {nullptr, nullptr};            // a slot's chunk walked (and its block read back)
@@ -952,7 +948,7 @@ int gpd_decode_host(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out) {
     s.hi = j;
     s.busy = true;
     i = j;
-    k = (k + 1) % kHostSlots;
+    k ^= 1;
   }
   for (auto &s : ctx->slot) {
     if (s.busy) {
@@ -969,6 +965,47 @@ int gpd_host_register(gpd_ctx *ctx, const void *ptr, uint64_t len) {
   HIP_TRY(hipSetDevice(ctx->device));
   HIP_TRY(hipHostRegister(const_cast<void *>(ptr), len, hipHostRegisterDefault));
   ctx->registered.emplace_back((const uint8_t *)ptr, len);
+  return GPD_OK;
+}
+
+// The NUMA node of a device's PCI function (sysfs), -1 when unknown.
+static int device_numa_node(int device) {
+  char bus[64] = {0};
+  int count = 0;
+  // (a failed HIP call would stay the thread's last error, and the caller's next launch check,
+  // torch's included, would report it: clear it)
+  if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count ||
+      hipDeviceGetPCIBusId(bus, (int)sizeof bus - 1, device) != hipSuccess) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  for (char *c = bus; *c; c++) *c = (char)tolower((unsigned char)*c);
+  char path[160];
+  std::snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/numa_node", bus);
+  FILE *f = std::fopen(path, "r");
+  if (!f) return -1;
+  int node = -1;
+  if (std::fscanf(f, "%d", &node) != 1) node = -1;
+  std::fclose(f);
+  return node;
+}
+
+int gpd_host_bind_local(int device, void *ptr, uint64_t len, int *node_out) {
+  if (node_out) *node_out = -1;
+  if (!ptr || !len) return set_err(GPD_ERR_INVALID, "gpd_host_bind_local: bad argument");
+  const int node = device_numa_node(device);
+  if (node_out) *node_out = node;
+  if (node < 0) return GPD_OK;  // one node, or the platform does not say
+  if (node >= 1024) return set_err(GPD_ERR_INVALID, "gpd_host_bind_local: node %d", node);
+  const uint64_t page = (uint64_t)sysconf(_SC_PAGESIZE);
+  const uint64_t lo = ((uint64_t)ptr + page - 1) & ~(page - 1), hi = ((uint64_t)ptr + len) & ~(page - 1);
+  if (hi <= lo) return GPD_OK;
+  unsigned long mask[1024 / (8 * sizeof(unsigned long))] = {0};
+  mask[node / (8 * sizeof(unsigned long))] = 1ul << (node % (8 * sizeof(unsigned long)));
+  // MPOL_PREFERRED (1): the node while it has free pages; MPOL_MF_MOVE (2): migrate pages
+  // already placed elsewhere
+  if (syscall(SYS_mbind, (void *)lo, hi - lo, 1, mask, (unsigned long)(8 * sizeof mask), 2u) != 0)
+    return set_err(GPD_ERR_INVALID, "gpd_host_bind_local: mbind: %s", std::strerror(errno));
   return GPD_OK;
 }
 
@@ -1047,8 +1084,6 @@ static int decode_pcap_host_walk(gpd_ctx *ctx, const uint8_t *buf, uint64_t len,
     std::string err;
   };
   static thread_local Part part[2];
-  const double t_call = now_ms();
-  g_pt_walk = g_pt_walkwait = g_pt_stage = g_pt_sync = g_pt_drain = 0;
   double walk_ms = 0;  // (written by the walking thread, read after its join)
   auto walk_part = [&](Part &P, uint64_t at, uint64_t m) {
     const double t0 = now_ms();
@@ -1134,7 +1169,7 @@ static int decode_pcap_host_walk(gpd_ctx *ctx, const uint8_t *buf, uint64_t len,
       s.hi = done + j;
       s.busy = true;
       i = j;
-      k = (k + 1) % kHostSlots;
+      k ^= 1;
     }
     done += n;
     *n_out = done;
@@ -1166,8 +1201,7 @@ static int decode_pcap_host_walk(gpd_ctx *ctx, const uint8_t *buf, uint64_t len,
       g_pt_drain += now_ms() - t1;
     }
   }
-  g_pt_walk = walk_ms;
-  g_pt_total = now_ms() - t_call;
+  g_pt_walk += walk_ms;
   return GPD_OK;
 }
 
@@ -1318,6 +1352,25 @@ static int decode_device_walk(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, co
   return GPD_OK;
 }
 
+// Records whose header starts in [pos, pos + span), as the ReadPacketData loop finds them, up to
+// the first one it would reject (the host walk then stops there with the reference's error).
+static uint64_t count_records(const uint8_t *buf, uint64_t len, const gpd_pcap_info &I, uint64_t pos,
+                              uint64_t span, uint64_t max_n) {
+  auto rd = [&](uint64_t p) {
+    uint32_t v;
+    std::memcpy(&v, buf + p, 4);
+    return I.big_endian ? __builtin_bswap32(v) : v;
+  };
+  uint64_t n = 0, p = pos;
+  while (n < max_n && p < pos + span && p + GPD_PCAP_RECORD_BYTES <= len) {
+    const uint32_t cap = rd(p + 8), wire = rd(p + 12);
+    if (cap > I.snaplen || cap > wire || p + GPD_PCAP_RECORD_BYTES + cap > len) break;
+    p += GPD_PCAP_RECORD_BYTES + cap;
+    n++;
+  }
+  return n;
+}
+
 int gpd_decode_pcap_at(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, const gpd_pcap_info *info,
                        uint64_t pos, uint64_t max_n, const gpd_result *out, uint64_t *n_out,
                        uint64_t *next_pos, int *stop, int nthreads) {
@@ -1333,34 +1386,58 @@ int gpd_decode_pcap_at(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, const gpd
   if (max_n == 0) return GPD_OK;
   HIP_TRY(hipSetDevice(ctx->device));
   const double t_call = now_ms();
+  g_pt_walk = g_pt_walkwait = g_pt_stage = g_pt_sync = g_pt_drain = 0;
+  struct Total {
+    double t;
+    ~Total() { g_pt_total = now_ms() - t; }
+  } total{t_call};
+  const bool dw = ctx->tune.device_walk != 0;
   uint64_t done = 0, at = pos;
-  if (ctx->tune.device_walk != 0) {
-    uint64_t resume;
-    const int rc = decode_device_walk(ctx, buf, len, *info, pos, max_n, out, nthreads, &done, &resume,
-                                           next_pos, stop);
-    if (rc) return rc;
-    if (resume == UINT64_MAX) {
+  auto shifted = [&](uint64_t d) {
+    gpd_result r = *out;
+    auto sh = [&](auto *p) { return p ? p + d : p; };
+    r.status = sh(out->status);
+    r.layers = sh(out->layers);
+    r.net_hash = sh(out->net_hash);
+    r.tp_hash = sh(out->tp_hash);
+    r.csum = sh(out->csum);
+    r.hdr_off = sh(out->hdr_off);
+    r.detail = sh(out->detail);
+    return r;
+  };
+  for (;;) {
+    if (dw) {
+      uint64_t resume, handled = 0;
+      const gpd_result r = shifted(done);
+      const int rc = decode_device_walk(ctx, buf, len, *info, at, max_n - done, &r, nthreads, &handled,
+                                        &resume, next_pos, stop);
+      done += handled;
       *n_out = done;
-      g_pt_walk = g_pt_walkwait = g_pt_stage = g_pt_sync = g_pt_drain = 0;
-      g_pt_total = now_ms() - t_call;
-      return GPD_OK;
+      if (rc) return rc;
+      if (resume == UINT64_MAX) return GPD_OK;
+      at = resume;
     }
-    at = resume;
+    // The host walk from `at`: all of the call without the device walk; else only the chunk
+    // the device walk could not vouch for (a record the reference rejects, a capture ending
+    // inside a record, a speculation its stitch refuted), and then the device walk again
+    // (one refuted speculation used to send the rest of the call to the host walk: r04, a
+    // 2^24-record replay call 28 -> 200 ms)
+    uint64_t lim = max_n - done;
+    if (dw) {
+      constexpr uint64_t kSpan = (uint64_t)gpd::kPwSeg * gpd::kPwMaxSeg;  // the device walk's chunk
+      lim = std::min(lim, count_records(buf, len, *info, at, kSpan, lim) + 1u);
+    }
+    const gpd_result r = shifted(done);
+    uint64_t k = 0, nxt = at;
+    int st = GPD_PCAP_STOP_LIMIT;
+    const int rc = decode_pcap_host_walk(ctx, buf, len, info, at, lim, &r, &k, &nxt, &st, nthreads);
+    done += k;
+    *n_out = done;
+    if (next_pos) *next_pos = nxt;
+    if (stop) *stop = st;
+    if (rc || !dw || st != GPD_PCAP_STOP_LIMIT || done == max_n) return rc;
+    at = nxt;
   }
-  // the host walk from `at` (all of the call, or what the device walk left)
-  gpd_result rest = *out;
-  auto shift = [&](auto *p) { return p ? p + done : p; };
-  rest.status = shift(out->status);
-  rest.layers = shift(out->layers);
-  rest.net_hash = shift(out->net_hash);
-  rest.tp_hash = shift(out->tp_hash);
-  rest.csum = shift(out->csum);
-  rest.hdr_off = shift(out->hdr_off);
-  rest.detail = shift(out->detail);
-  uint64_t k = 0;
-  const int rc = decode_pcap_host_walk(ctx, buf, len, info, at, max_n - done, &rest, &k, next_pos, stop, nthreads);
-  *n_out = done + k;
-  return rc;
 }
 
 void gpd_decode_pcap_last_times(double *ms6) {

@@ -23,7 +23,8 @@
  *                     tcpassembly/assembly.go:193-200)
  *   gpd_flow_reset / gpd_flow_destroy                    (pool lifetime)
  *
- * The table is open addressing in HBM: 2^k records of 80 bytes; a record is claimed by a
+ * The table is open addressing in HBM: 2^k slots of 80 bytes (a 64-byte line of what every
+ * packet of the flow reads and updates, and 16 bytes of `first` and counter spills); a record is claimed by a
  * 56-bit fingerprint of its key (tagged with the claiming call's epoch) with one
  * compare-and-swap, and every packet's full key is compared with the record's stored key — at
  * once for records of earlier calls, in a second pass for records claimed in the same call —
@@ -38,7 +39,8 @@
 extern "C" {
 #endif
 
-/* One flow record (80 B, device memory; gpd_flow_export copies occupied ones out). */
+/* One flow record as gpd_flow_export copies it out (80 B; the table keeps the same fields as
+ * a 64-byte and a 16-byte record per slot). */
 typedef struct gpd_flow_rec {
   uint64_t fp;          /* key fingerprint (56 bits); 0 = empty record */
   uint8_t  src[16];     /* NetworkFlow().Src() raw bytes (4 used for IPv4) */

@@ -21,6 +21,8 @@
  *                         gpd_decode + D2H, double-buffered
  *   gpd_host_register     (no reference counterpart) pin a caller buffer so the H2D of
  *                         gpd_decode_pcap reads it in place
+ *   gpd_host_bind_local   (no reference counterpart) put a caller buffer's pages on the GPU's
+ *                         NUMA node
  *
  * gzip-compressed captures (pcapgo/read.go:79-86) are inflated by the caller (the Python
  * layer does it transparently); the walker sees uncompressed bytes.
@@ -141,6 +143,13 @@ void gpd_pcap_last_stats(int *threads, int *met, int *rewalks);
 /* Pin / unpin host memory for in-place H2D (hipHostRegister on the context's device). */
 int gpd_host_register(gpd_ctx *ctx, const void *ptr, uint64_t len);
 int gpd_host_unregister(gpd_ctx *ctx, const void *ptr);
+
+/* Place host memory on the NUMA node of device `device`'s PCI function (mbind, preferred
+ * policy, over the whole pages of [ptr, ptr + len); pages already placed elsewhere move).  A
+ * capture buffer there reaches the GPU without crossing the link between sockets; bound before
+ * its pages are first written, nothing moves.  *node (may be NULL): the node, or -1 when the
+ * platform names none (then nothing is done and GPD_OK is returned). */
+int gpd_host_bind_local(int device, void *ptr, uint64_t len, int *node);
 
 #ifdef __cplusplus
 }

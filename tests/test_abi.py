@@ -27,7 +27,7 @@ def test_header_declares_the_boundary():
     fns = declared_functions()
     for f in ("gpd_ctx_create", "gpd_decode", "gpd_decode_host", "gpd_sync", "gpd_ctx_destroy",
               "gpd_last_error_string", "gpd_ctx_reload_tables", "gpd_default_tables",
-              "gpd_pcap_header", "gpd_pcap_index", "gpd_decode_pcap", "gpd_host_register",
+              "gpd_pcap_header", "gpd_pcap_index", "gpd_decode_pcap", "gpd_host_register", "gpd_host_bind_local",
               "gpd_flow_create", "gpd_flow_insert", "gpd_flow_export", "gpd_flow_stats_get",
               "gpd_ip4_fragments"):
         assert f in fns

@@ -117,3 +117,34 @@ def test_fast_path_leaves_no_fragment_to_the_fallback():
     # only the cut / odd frames may fall back: every whole fragment is a fast-path decode
     whole = sum(1 for i in range(b.n) if (int(ref.status[i]) & 3) == 0)
     assert fb.value <= b.n - whole
+
+
+def test_host_bind_local_places_pages_on_the_gpu_node():
+    """gpd_host_bind_local: a fresh buffer bound before its first write has its pages on the
+    GPU's NUMA node (sysfs numa_node of its PCI function); -1 / no-op where none is named."""
+    import mmap
+
+    import torch
+    from gopacket_amd._lib import lib
+    torch.cuda.init()
+    n = 64 << 20
+    mm = mmap.mmap(-1, n)
+    a = np.frombuffer(mm, np.uint8)
+    node = C.c_int(-2)
+    assert lib.gpd_host_bind_local(0, a.ctypes.data, n, C.byref(node)) == 0, lib.gpd_last_error_string()
+    a[::4096] = 1  # first touch
+    if node.value < 0:
+        pytest.skip("the platform names no NUMA node for the GPU")
+    pages = {}
+    lo, hi = a.ctypes.data, a.ctypes.data + n
+    with open("/proc/self/numa_maps") as f:
+        for line in f:
+            if lo - 4096 <= int(line.split()[0], 16) < hi:
+                for tok in line.split()[1:]:
+                    if tok[0] == "N" and "=" in tok:
+                        k, v = tok.split("=")
+                        pages[int(k[1:])] = pages.get(int(k[1:]), 0) + int(v)
+    assert pages, "buffer not found in numa_maps"
+    assert pages.get(node.value, 0) >= 0.9 * sum(pages.values()), (node.value, pages)
+    del a
+    mm.close()

@@ -158,6 +158,44 @@ def test_flow_table_accumulates_and_resets():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("order", ["ascending", "descending", "same_base_twice"])
+def test_flow_table_sequence_bases_in_any_order(order):
+    """A record of an earlier call skips its `first` update only when the packet's sequence
+    number is above every earlier call's (the host's bound, FlowParams::seen): batches inserted
+    with descending index bases (first must still fall) or the same base twice are exact."""
+    import torch
+    from gopacket_amd import flows as FL
+    from gopacket_amd import parser as P
+    a, b = _hot_batch(7000, 300, 3), _hot_batch(5000, 300, 4)
+    parser = P.NewDecodingLayerParser(L.LayerTypeEthernet, P.Ethernet(), P.Dot1Q(), P.IPv4(), P.IPv6(),
+                                      P.TCP(), P.UDP(), P.VXLAN(), P.Payload())
+    ft = FL.NewFlowTable(parser, 1 << 12)
+    steps = {"ascending": [(a, 0), (b, a.n)], "descending": [(b, a.n), (a, 0)],
+             "same_base_twice": [(a, 0), (a, 0)]}[order]
+    ids = {}
+    for batch, base in steps:
+        db, dr = _decode_dev(parser, batch)
+        ids.setdefault(base, []).append(ft.Insert(db, dr, index_base=base).cpu().numpy().view(np.uint32))
+    torch.cuda.synchronize()
+    if order == "same_base_twice":
+        # twice the same packets at the same sequence numbers: the records hold every packet twice
+        both = PacketBatch.from_packets([a.packet(i) for i in range(a.n)] * 2)
+        ref = O.decode(both, L.LayerTypeEthernet, parser.decoders, 0, ext=False, nthreads=8)
+        flows_ref, per_ref = F.group(both, ref)
+        ex, _ = ft.Export()
+        assert len(ex) == len(flows_ref)
+        for r in ex:
+            f = flows_ref[F.record_key(r)]
+            assert (int(r["first"]), int(r["last"]), int(r["packets"]), int(r["bytes"])) == \
+                (f["first"], f["last"] - a.n, f["packets"], f["bytes"])
+        return
+    both = PacketBatch.from_packets([a.packet(i) for i in range(a.n)] + [b.packet(i) for i in range(b.n)])
+    ref = O.decode(both, L.LayerTypeEthernet, parser.decoders, 0, ext=False, nthreads=8)
+    flows_ref, per_ref = F.group(both, ref)
+    _check_table(both, None, np.concatenate([ids[0][0], ids[a.n][0]]), ft, flows_ref, per_ref)
+
+
+@pytest.mark.gpu
 def test_flow_table_full():
     """More distinct keys than records: every lane leaves its probe loop; the overflow is
     counted and flagged, the records that exist stay exact."""

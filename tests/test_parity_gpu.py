@@ -392,6 +392,23 @@ def test_round_kernel_long_segments(waves):
         run_both(PacketBatch.from_packets(pk, align=align), ext=False, tuning=t)
 
 
+@pytest.mark.parametrize("align", [16, 4, 1])
+def test_round_kernel_short_segments_in_long_frames(align):
+    """ro_kernel: IMIX frames padded with trailing bytes to 129 B .. 9 KB (the IP length keeps
+    the segment short, so it can end in the round before the one the frame's 128 header bytes
+    reach: summed from the carried bytes and prefix words), among unpadded frames, against the
+    oracle.  The r04 device-walk capture test found such a frame summed from a wrong prefix."""
+    rng = np.random.default_rng(0x5EED0611 + align)
+    base = synth.make_imix(1 << 13, seed=0x5EED0612)
+    pk = [base.packet(i) for i in range(base.n)]
+    for i in rng.choice(len(pk), size=len(pk) // 8, replace=False):
+        want = int(rng.choice([129, 200, 1600, 8200, 9000]))
+        if len(pk[i]) < want:
+            pk[i] = pk[i] + bytes(rng.integers(0, 256, want - len(pk[i]), dtype=np.uint8))
+    for ho in (2, 1):
+        run_both(PacketBatch.from_packets(pk, align=align), ext=False, tuning=dict(header_once=ho))
+
+
 def test_layouts_unaligned_shuffled_large_empty():
     pk = _golden_packets() + [b"", b"\x01", b"\x00" * 13]
     big = [G.case_bytes(c) for c in CASES if c["name"] == "ipv6_jumbogram_dlp"][0]

@@ -1,9 +1,11 @@
 #!/bin/bash
-# A/B of the F3 flow insert on one box: ab_old/ (an earlier commit, tools/ab_lib.sh) against the
-# working tree, alternating, two rounds; prints insert_ms (new flows) and existing_flows.insert_ms.
-# usage: bash tools/ab_flows.sh
+# A/B of the F3 flow insert on one box: trees (each with its own built libgpd.so; default
+# ab_old/ against the working tree), alternating, two rounds; prints insert_ms (new flows),
+# existing_flows.insert_ms and bursts16.insert_ms.
+# usage: bash tools/ab_flows.sh [DIR ...]
 set -e
 mkdir -p gpurun_out/ab
+[ $# -gt 0 ] || set -- ab_old .
 run() { tag=$1; dir=$2; (cd $dir && timeout -k 10 200 python bench.py --no-cpu-baseline --lean --steps 10 --flows) > gpurun_out/ab/$tag.log 2>&1; python -c "
 import json
 for l in open('gpurun_out/ab/$tag.log'):
@@ -11,6 +13,5 @@ for l in open('gpurun_out/ab/$tag.log'):
         d = json.loads(l); b = d.get('bursts16', {})
         print('$tag', d['insert_ms'], d['existing_flows']['insert_ms'], b.get('insert_ms', b), flush=True)"; }
 for k in 1 2; do
-  run flows_prev$k ab_old
-  run flows_new$k .
+  for t in "$@"; do run flows_$(basename $(realpath $t))$k $t; done
 done
