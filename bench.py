@@ -932,6 +932,8 @@ def bench_replay(args, world, rank, local, dist):
     # where the time of the PCIe-inclusive leg goes: each call's wall time and its phases
     # (gpd_decode_pcap_last_times: walk, staging, waits for the slots' transfers + decode, drain)
     call_ms, phases, call_ph = [], np.zeros(6, np.float64), []
+    wc, walk_counts = np.zeros(7, np.uint32), np.zeros(7, np.int64)
+    wm, misses = np.zeros(2, np.uint64), []
     ph = np.zeros(6, np.float64)
     t0 = time.perf_counter()
     p, done, last = start, 0, 0
@@ -941,7 +943,12 @@ def bench_replay(args, world, rank, local, dist):
                                               data_len=end)
         call_ms.append((time.perf_counter() - tc) * 1e3)
         lib.gpd_decode_pcap_last_times(ph.ctypes.data)
+        lib.gpd_decode_pcap_last_walk_counts(wc.ctypes.data)
+        if wc[1] or wc[6]:
+            lib.gpd_decode_pcap_last_walk_miss(wm.ctypes.data)
+            misses.append([int(wm[0]), int(wm[1])])
         phases += ph
+        walk_counts += wc
         call_ph.append(ph.copy())
         assert err is None and k > 0, err
         done += k
@@ -957,6 +964,11 @@ def bench_replay(args, world, rank, local, dist):
                  "phases_ms_total": dict(zip(["total", "walk", "walk_wait", "stage", "sync", "drain"],
                                              [round(float(x), 1) for x in phases])),
                  "capture_placement": host_placement(cap, local), "numa_bind": rc.bind}
+    pcie_diag["device_walk_chunks"] = dict(zip(
+        ["walked", "to_host", "speculation_refuted", "record_rejected", "header_uncovered", "walk_short",
+         "segments_rewalked_on_device"],
+        [int(x) for x in walk_counts]))
+    pcie_diag["device_walk_misses"] = misses[:16]  # [start, segment] capture positions
     names = ["total", "walk", "walk_wait", "stage", "sync", "drain"]
     pcie_diag["slowest_calls"] = [
         {"call": int(j), "ms": round(float(cm[j]), 2),

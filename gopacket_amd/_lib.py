@@ -79,6 +79,8 @@ EXPORTS = {
                                   C.POINTER(C.c_int), C.c_int]),
     "gpd_pcap_last_stats": (None, [C.POINTER(C.c_int)] * 3),
     "gpd_decode_pcap_last_times": (None, [C.c_void_p]),
+    "gpd_decode_pcap_last_walk_counts": (None, [C.c_void_p]),
+    "gpd_decode_pcap_last_walk_miss": (None, [C.c_void_p]),
     "gpd_host_register": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
     "gpd_host_unregister": (C.c_int, [C.c_void_p, C.c_void_p]),
     "gpd_host_bind_local": (C.c_int, [C.c_int, C.c_void_p, C.c_uint64, C.POINTER(C.c_int)]),

@@ -96,7 +96,11 @@ struct PwCtl {       // a chunk's control block (device; copied back to the host
   uint32_t entry;    // in: its first record header (relative to the chunk)
   uint32_t n;        // out: records whose headers start in [entry, own_end)
   uint32_t next;     // out: the first record header at or past own_end
-  uint32_t status;   // out: 0, or 1 = the host walks from `entry` (see gpd_pcapwalk.hip)
+  uint32_t status;   // out: 0, or 1 | reasons (2 speculation refuted, 4 rejected record, 8 header
+                     // not covered, 16 walk ends short) = the host walks from `entry` (gpd_pcapwalk.hip)
+  uint32_t miss_st;  // out (diagnostic): the first refuted speculation's start ...
+  uint32_t miss_at;  // ... and its segment (kNone: none)
+  uint32_t pad[2];   // [0]: segments the stitch re-walked from the true walk's position
 };
 struct PwArgs {
   const uint8_t *d;        // the chunk's bytes in HBM

@@ -1747,6 +1747,9 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void decode_kernel(KParams P) {
 template <uint32_t K>
 __device__ __forceinline__ void decode_fallback_list(const KParams &P, uint32_t buf, uint32_t fb_start, uint32_t fb_c,
                                                      uint32_t lane, uint32_t dlen, uint32_t options) {
+#if GPD_EXP & 8
+  return;  // (A/B diagnostic build, tools/mix_diag.sh: the generic decodes skipped, wrong results)
+#endif
   if (fb_c) {
     __threadfence_block();  // the entries other lanes of this wave stored
     const Tab<false> T{P.pages,    P.eth_base, P.tcp_base, P.udp_base, P.eth_bits,

@@ -139,52 +139,118 @@ __global__ __launch_bounds__(256) void pw_walk(PwArgs A) {
   A.bad[s] = bad;
 }
 
-// One workgroup of 1024 lanes; lane t owns segments [t*R, t*R + R).
+// One workgroup of 1024 lanes; lane t owns segments [t*R, t*R + R).  Where the true walk
+// disagrees with a segment's speculation (it enters the segment elsewhere, or enters one whose
+// scan found no start), the owning lane re-walks that segment from where the true walk stands,
+// and the check runs again (a fix can move where the next lane's first segment is entered):
+// up to kFixRounds rounds, after which the chunk is the host's.  Payload bytes that read as a
+// chain of plausible headers (config 5's 64-B records: a view 3 bytes into each record chains
+// 16,400-byte "records" forever) then cost a few microseconds of this workgroup instead of a
+// host walk of the chunk.
+constexpr int kFixRounds = 4;
+
+__device__ __forceinline__ void pw_rewalk(const PwArgs &A, uint32_t s, uint32_t at, uint32_t hi) {
+  if (at >= hi) {  // a longer record covers the whole segment: no header starts in it
+    A.st[s] = kNone;
+    A.ct[s] = 0;
+    A.bad[s] = 0;
+    return;
+  }
+  uint32_t p = at, cnt = 0, bad = 0;
+  while (p < hi) {
+    uint32_t cap;
+    if (!pw_step(A, p, cap)) {
+      bad = 1;
+      break;
+    }
+    cnt++;
+    p += 16u + cap;
+  }
+  A.st[s] = at;
+  A.ex[s] = p;
+  A.ct[s] = cnt;
+  A.bad[s] = bad;
+}
+
 __global__ __launch_bounds__(1024) void pw_stitch(PwArgs A) {
-  __shared__ uint32_t s_cnt[1024], s_last[1024], s_ok[1024];
+  __shared__ uint32_t s_cnt[1024], s_last[1024], s_ok[1024], s_fixed, s_nfix;
+  __shared__ unsigned long long s_miss;  // the first refuted segment << 32 | its speculated start
   const uint32_t t = threadIdx.x;
   const uint32_t R = (A.nseg + 1023u) / 1024u;
   const uint32_t a = min(t * R, A.nseg), b = min(a + R, A.nseg);
-  uint32_t cnt = 0, last = kNone;  // this lane's record count and last segment that found a start
-  for (uint32_t s = a; s < b; s++) {
-    if (A.st[s] != kNone) {
-      cnt += A.ct[s];
-      last = s;
-    }
-  }
-  s_cnt[t] = cnt;
-  s_last[t] = last;
-  __syncthreads();
-  // inclusive scans across lanes (Hillis-Steele; 1024 entries): + of counts, max of last
-  for (uint32_t d = 1; d < 1024u; d <<= 1) {
-    const uint32_t c = t >= d ? s_cnt[t - d] : 0u;
-    const uint32_t l = t >= d ? s_last[t - d] : kNone;
-    __syncthreads();
-    s_cnt[t] += c;
-    if (l != kNone && (s_last[t] == kNone || l > s_last[t])) s_last[t] = l;
-    __syncthreads();
-  }
-  uint32_t base = t ? s_cnt[t - 1] : 0u;
-  uint32_t prev = t ? s_last[t - 1] : kNone;  // the last segment with a start before a
   const uint32_t e = A.ctl->entry;
-  uint32_t ok = 1;
-  for (uint32_t s = a; s < b; s++) {
-    const uint32_t lo = s * kPwSeg, hi = min(lo + kPwSeg, A.own_end);
-    // where the true walk stands when it reaches this segment
-    const uint32_t at = prev == kNone ? e : A.ex[prev];
-    if (A.st[s] != kNone) {
-      if (A.st[s] != at || A.bad[s]) ok = 0;  // a speculation the true walk misses, a rejected record
-      A.base[s] = base;
-      base += A.ct[s];
-      prev = s;
-    } else if (at < hi && at >= lo) {
-      ok = 0;  // a record header of the true walk starts here, and no walk covered it
-    }
+  if (t == 0) {
+    s_miss = ~0ull;
+    s_nfix = 0;
   }
-  s_ok[t] = ok;
+  uint32_t why = 0;  // the host's reasons (PwCtl::status bits), 0 = the walk stands
+  for (int round = 0;; round++) {
+    uint32_t cnt = 0, last = kNone;  // this lane's record count and last segment that found a start
+    for (uint32_t s = a; s < b; s++) {
+      if (A.st[s] != kNone) {
+        cnt += A.ct[s];
+        last = s;
+      }
+    }
+    s_cnt[t] = cnt;
+    s_last[t] = last;
+    if (t == 0) s_fixed = 0;
+    __syncthreads();
+    // inclusive scans across lanes (Hillis-Steele; 1024 entries): + of counts, max of last
+    for (uint32_t d = 1; d < 1024u; d <<= 1) {
+      const uint32_t c = t >= d ? s_cnt[t - d] : 0u;
+      const uint32_t l = t >= d ? s_last[t - d] : kNone;
+      __syncthreads();
+      s_cnt[t] += c;
+      if (l != kNone && (s_last[t] == kNone || l > s_last[t])) s_last[t] = l;
+      __syncthreads();
+    }
+    uint32_t base = t ? s_cnt[t - 1] : 0u;
+    uint32_t prev = t ? s_last[t - 1] : kNone;  // the last segment with a start before a
+    uint32_t fixed = 0;
+    why = 0;
+    for (uint32_t s = a; s < b; s++) {
+      const uint32_t lo = s * kPwSeg, hi = min(lo + kPwSeg, A.own_end);
+      // where the true walk stands when it reaches this segment
+      const uint32_t at = prev == kNone ? e : A.ex[prev];
+      uint32_t st = A.st[s];
+      const bool refuted = st != kNone && st != at;             // a speculation the true walk misses
+      const bool uncovered = st == kNone && at >= lo && at < hi;  // a header of the true walk, unwalked
+      if (refuted || uncovered) {
+        if (round < kFixRounds) {
+          if (refuted) atomicMin(&s_miss, ((unsigned long long)s << 32) | st);
+          // (`at` below the segment: the previous lane is fixing a segment of its own in this
+          // round, and the next round sees where the walk really enters this one)
+          if (at >= lo) {
+            pw_rewalk(A, s, at, hi);
+            st = A.st[s];
+          }
+          fixed++;
+        } else {
+          why |= refuted ? 2u : 8u;
+        }
+      }
+      if (st != kNone) {
+        if (A.bad[s]) why |= 4u;  // a record the reference rejects (or cut by the bytes)
+        A.base[s] = base;
+        base += A.ct[s];
+        prev = s;
+      }
+    }
+    if (fixed) {
+      s_fixed = 1u;
+      atomicAdd(&s_nfix, fixed);
+    }
+    __threadfence_block();  // (the re-walked segments' words, for the other lanes' next round)
+    __syncthreads();
+    const bool again = s_fixed != 0u;
+    __syncthreads();
+    if (!again) break;
+  }
+  s_ok[t] = why;
   __syncthreads();
   for (uint32_t d = 512; d > 0; d >>= 1) {
-    if (t < d) s_ok[t] &= s_ok[t + d];
+    if (t < d) s_ok[t] |= s_ok[t + d];
     __syncthreads();
   }
   if (t == 1023u) {
@@ -194,10 +260,14 @@ __global__ __launch_bounds__(1024) void pw_stitch(PwArgs A) {
     // a capture that does not end exactly after a record (or a chunk whose walk stopped short
     // of its end) is the host's to walk
     const bool done = A.last ? next == A.T : next >= A.own_end;
-    const bool good = s_ok[0] && done;
+    const uint32_t why_all = s_ok[0] | (done ? 0u : 16u);  // 16: the walk ends short of the bytes
+    A.ctl->miss_st = s_miss == ~0ull ? kNone : (uint32_t)s_miss;
+    A.ctl->miss_at = s_miss == ~0ull ? kNone : (uint32_t)(s_miss >> 32);
+    A.ctl->pad[0] = s_nfix;  // segments re-walked here
+    const bool good = why_all == 0u;
     A.ctl->n = good ? total : 0u;
     A.ctl->next = next;
-    A.ctl->status = good ? 0u : 1u;
+    A.ctl->status = good ? 0u : 1u | why_all;
     if (good && A.ctl_next) A.ctl_next->entry = next - A.own_end;
   }
 }

@@ -1043,6 +1043,9 @@ static void par_memcpy(uint8_t *dst, const uint8_t *src, uint64_t n, int nthread
 // Host-clock phases of this thread's last gpd_decode_pcap(_at) call (gpd_decode_pcap_last_times).
 static thread_local double g_pt_walk = 0, g_pt_walkwait = 0, g_pt_stage = 0, g_pt_sync = 0, g_pt_drain = 0,
                            g_pt_total = 0;
+// ... and its device-walk chunks: walked, handed to the host, and the reasons (PwCtl::status bits)
+static thread_local uint32_t g_pw_counts[7];
+static thread_local uint64_t g_pw_miss[2] = {~0ull, ~0ull};  // the last refuted speculation: start, segment
 static double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -1066,7 +1069,12 @@ static int decode_pcap_host_walk(gpd_ctx *ctx, const uint8_t *buf, uint64_t len,
   if (next_pos) *next_pos = pos;
   if (stop) *stop = GPD_PCAP_STOP_LIMIT;
   if (max_n == 0) return GPD_OK;
-  const uint64_t kPkts = 1u << 20, kBytes = 256ull << 20;
+  const uint64_t kPkts = 1u << 20;
+  // staging chunks of up to 256 MiB; slots of 64 MiB or more that the device walk already holds
+  // serve as they are when a record fits them (a stretch the device walk hands over: pinned
+  // slots re-allocated in the middle of a replay cost ~130 ms, r04)
+  const uint64_t kBytes = ctx->slot_bytes >= (64ull << 20) && ctx->slot_bytes >= 64ull + info->snaplen
+                              ? std::min<uint64_t>(ctx->slot_bytes, 256ull << 20) : 256ull << 20;
   const uint64_t kPart = 1u << 21;  // records per walked part (the first, walked before any
   const uint64_t kPart0 = 1u << 19; // transfer can start, is smaller)
   int rc = alloc_slots(ctx, kBytes, kPkts, false, out->detail != nullptr);
@@ -1309,7 +1317,15 @@ static int decode_device_walk(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, co
     if (ahead && (rc = issue(k + 1, B + own, 0))) return rc;
     HIP_TRY(hipEventSynchronize(ctx->ev_pw[k & 1]));  // chunk k walked: its count
     const gpd::PwCtl c = ctx->h_pw_ctl[k & 1];
-    if (c.status != 0) {  // the host walks from this chunk's entry (its decode saw 0 records)
+    g_pw_counts[0]++;
+    g_pw_counts[6] += c.pad[0];
+    if (c.miss_at != 0xFFFFFFFFu) {
+      g_pw_miss[0] = B + c.miss_st;
+      g_pw_miss[1] = B + (uint64_t)c.miss_at * gpd::kPwSeg;
+    }
+    if (c.status != 0) {
+      g_pw_counts[1]++;
+      for (int b = 0; b < 4; b++) g_pw_counts[2 + b] += (c.status >> (b + 1)) & 1u;  // the host walks from this chunk's entry (its decode saw 0 records)
       *resume = B + entry;
       break;
     }
@@ -1387,6 +1403,8 @@ int gpd_decode_pcap_at(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, const gpd
   HIP_TRY(hipSetDevice(ctx->device));
   const double t_call = now_ms();
   g_pt_walk = g_pt_walkwait = g_pt_stage = g_pt_sync = g_pt_drain = 0;
+  for (auto &c : g_pw_counts) c = 0;
+  g_pw_miss[0] = g_pw_miss[1] = ~0ull;
   struct Total {
     double t;
     ~Total() { g_pt_total = now_ms() - t; }
@@ -1438,6 +1456,17 @@ int gpd_decode_pcap_at(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, const gpd
     if (rc || !dw || st != GPD_PCAP_STOP_LIMIT || done == max_n) return rc;
     at = nxt;
   }
+}
+
+void gpd_decode_pcap_last_walk_miss(uint64_t *pos2) {
+  if (!pos2) return;
+  pos2[0] = g_pw_miss[0];
+  pos2[1] = g_pw_miss[1];
+}
+
+void gpd_decode_pcap_last_walk_counts(uint32_t *c7) {
+  if (!c7) return;
+  for (int k = 0; k < 7; k++) c7[k] = g_pw_counts[k];
 }
 
 void gpd_decode_pcap_last_times(double *ms6) {

@@ -136,6 +136,16 @@ int gpd_pcap_locate(const uint8_t *buf, uint64_t len, const gpd_pcap_info *info,
  * copying results out. */
 void gpd_decode_pcap_last_times(double *ms6);
 
+/* Diagnostics: this thread's last gpd_decode_pcap(_at) call's device-walk chunks — [0] walked,
+ * [1] handed to the host walk, and of those [2] a speculation the stitch could not correct,
+ * [3] a record the reader rejects (or one cut by the chunk's bytes), [4] a true record header
+ * no segment's walk covered, [5] a walk that ends short of the chunk; [6] 2-KiB segments the
+ * stitch re-walked from the true walk's position (a refuted speculation, corrected there). */
+void gpd_decode_pcap_last_walk_counts(uint32_t *c7);
+/* ... and where its last refuted speculation started and the 2-KiB segment it walked (buffer
+ * positions; UINT64_MAX when none). */
+void gpd_decode_pcap_last_walk_miss(uint64_t *pos2);
+
 /* Diagnostics of this thread's last walk: segments walked in parallel, segments whose
  * speculation the true walk met, segments re-walked sequentially. */
 void gpd_pcap_last_stats(int *threads, int *met, int *rewalks);

@@ -409,6 +409,70 @@ def test_round_kernel_short_segments_in_long_frames(align):
         run_both(PacketBatch.from_packets(pk, align=align), ext=False, tuning=dict(header_once=ho))
 
 
+def _vxlan_frames(rng):
+    """VXLAN frames in every outer shape fast_decode's first pass accepts or refuses, over inner
+    frames the round kernel's tile decode takes (Ethernet [Dot1Q] IPv4/IPv6 TCP/UDP) or leaves
+    to the generic decoder (no transport, inner IPv6 under outer IPv4, nested VXLAN, errors)."""
+    import struct
+
+    import error_sites as ES
+
+    def body(n):
+        return bytes(rng.integers(0, 256, n, dtype=np.uint8))
+
+    def vx(inner, outer="v4", tags=0, frag=0, udp_len=None, ip_len=None, pad=0, sport=40001, dport=4789):
+        u = ES.udp(b"\x08\x00\x00\x00\x00\x12\x34\x00" + inner, sport=sport, dport=dport, length=udp_len)
+        if outer == "v4":
+            l3, et = ES.ip4(u, proto=17, length=ip_len, flags_frag=frag), 0x0800
+        else:
+            l3, et = ES.ip6(u, nh=17, length=ip_len), 0x86DD
+        for _ in range(tags):
+            l3, et = struct.pack(">HH", 100, et) + l3, 0x8100
+        return ES.eth(et, l3) + bytes(pad)
+
+    inner = [ES.eth(0x0800, ES.ip4(ES.tcp(body(int(rng.integers(0, 300)))))),
+             ES.eth(0x0800, ES.ip4(ES.udp(body(40)), proto=17)),
+             ES.eth(0x86DD, ES.ip6(ES.tcp(body(24)))),
+             ES.eth(0x86DD, ES.ip6(ES.udp(body(9)), nh=17)),
+             ES.eth(0x8100, struct.pack(">HH", 7, 0x0800) + ES.ip4(ES.tcp(body(30)))),
+             ES.eth(0x0800, ES.ip4(ES.tcp(body(20), doff=7, opts=b"\x02\x04\x05\xb4\x01\x01\x01\x00"))),
+             ES.eth(0x0800, ES.ip4(ES.tcp(body(5), doff=4))),               # inner decode error
+             ES.eth(0x0800, ES.ip4(body(8), proto=1)),                      # ICMPv4: no transport
+             ES.eth(0x0806, body(28)),                                      # ARP: unsupported
+             ES.eth(0x0800, ES.ip4(ES.tcp(body(8)), ihl=6, opts=b"\x01\x01\x01\x00")),
+             ES.eth(0x0800, ES.ip4(ES.tcp(body(3000)))),                     # a long inner segment
+             ES.eth(0x0800, ES.ip4(ES.tcp(body(60)))[:50])]                   # inner frame cut
+    inner.append(vx(inner[0])[:])  # nested VXLAN
+    out = []
+    for inn in inner:
+        out += [vx(inn), vx(inn, outer="v6"), vx(inn, tags=1), vx(inn, tags=2), vx(inn, pad=30),
+                vx(inn, ip_len=20 + 8 + 8 + len(inn) + 40), vx(inn, frag=0x2000), vx(inn, udp_len=0),
+                vx(inn, udp_len=5), vx(inn, udp_len=8 + 8 + len(inn) + 10), vx(inn, sport=4789, dport=80),
+                vx(inn)[:14 + 20 + 8 + 8 + 20], vx(inn, outer="v6", tags=1, pad=3)]
+    out.append(vx(b""))   # VXLAN header only
+    out.append(vx(b"\x00" * 7))
+    return out
+
+
+@pytest.mark.parametrize("align", [16, 1])
+def test_vxlan_frame_shapes_in_every_kernel(align):
+    """Every outer and inner VXLAN shape above, among IMIX frames and config 4's VXLAN frames,
+    through the round kernel (which hands VXLAN frames to its wave's generic decoder), the
+    windowed header-once kernel (which decodes them per window) and the per-window kernels,
+    equals the oracle."""
+    rng = np.random.default_rng(0x5EED0621 + align)
+    base = synth.make_imix(1 << 12, seed=0x5EED0622)
+    vxb = synth.make_vxlan(1 << 11, seed=0x5EED0623)
+    pk = [base.packet(i) for i in range(base.n)] + [vxb.packet(i) for i in range(vxb.n)]
+    pk += _vxlan_frames(rng) * 3
+    order = rng.permutation(len(pk))
+    b = PacketBatch.from_packets([pk[i] for i in order], align=align)
+    for ho in (2, 1, 0):
+        run_both(b, ext=False, tuning=dict(header_once=ho))
+    run_both(b, ext=False, tuning=dict(header_once=2, waves_per_simd=2))
+    run_both(b, mask=0x3FF, options=1, ext=False, tuning=dict(header_once=2))
+
+
 def test_layouts_unaligned_shuffled_large_empty():
     pk = _golden_packets() + [b"", b"\x01", b"\x00" * 13]
     big = [G.case_bytes(c) for c in CASES if c["name"] == "ipv6_jumbogram_dlp"][0]

@@ -152,3 +152,26 @@ def test_device_walk_speculation_misses_fall_back():
     cap = NP.synth_capture(PacketBatch.from_packets(pk))
     n, err, _ = _both(cap)
     assert err is None and n == 60000
+
+
+def test_device_walk_corrects_refuted_speculation_on_device():
+    """Config 5's 64-B records, cut so that a 2-KiB walking segment starts 40 bytes into record
+    315870771: its scan finds a false chain 8 bytes before the next header (random payload
+    bytes that read as a sub-second fraction, then a view 3 bytes into every 205th record, which
+    chains 16,400-byte "records" forever).  The stitch re-walks that segment from the true walk's
+    position on the device (gpd_decode_pcap_last_walk_counts [6]) instead of handing the chunk to
+    the host walk ([1]), and every result equals the host walk's."""
+    from gopacket_amd._lib import lib
+    lo, n = 315870771 - 25, 100000
+    cap = np.zeros(24 + 80 * n + PAD, np.uint8)
+    cap[:24] = np.frombuffer(struct.pack("<IHHiIII", 0xA1B2C3D4, 2, 4, 0, 0, 262144, 1), np.uint8)
+    synth.udp64_native(cap[24:24 + 80 * n], lo, lo + n, 0x5EED0002, records=True, nthreads=8)
+    p = _parser(1)
+    _, k, err = p.DecodePcap(cap, nthreads=8)
+    wc = np.zeros(7, np.uint32)
+    lib.gpd_decode_pcap_last_walk_counts(wc.ctypes.data)
+    assert err is None and k == n
+    assert wc[1] == 0, wc      # no chunk went to the host walk
+    assert wc[6] >= 1, wc      # ... because the stitch corrected the segment itself
+    n2, err2, _ = _both(cap)
+    assert err2 is None and n2 == n
