@@ -1744,7 +1744,7 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void decode_kernel(KParams P) {
 // the (now idle) window buffer `buf` with independent 16-byte loads, so the decoder's dependent
 // header reads hit LDS (HybSrc); bytes past the slot (long segments) still come from global
 // memory.
-template <uint32_t K>
+template <uint32_t K, bool CS = true, bool HASH = true>
 __device__ __forceinline__ void decode_fallback_list(const KParams &P, uint32_t buf, uint32_t fb_start, uint32_t fb_c,
                                                      uint32_t lane, uint32_t dlen, uint32_t options) {
 #if GPD_EXP & 8
@@ -1771,9 +1771,15 @@ __device__ __forceinline__ void decode_fallback_list(const KParams &P, uint32_t 
                                               : v4u32{0u, 0u, 0u, 0u};
 #pragma unroll
       for (uint32_t k = 0; k < K / 16u; k++) *reinterpret_cast<v4u32 *>(g_lds + slot + 16u * k) = c[k];
-      if (live)
-        store_out(P, fi, decode_packet<false>(HybSrc<K>{P.data, off, gb, slot}, len, T, P.first, options, nullptr,
-                                              P.detail ? P.detail + fi : nullptr));
+      // a round whose packets all lie inside their slots reads LDS only (no per-read bound)
+      const bool all_in = __all(!live || (off & 15u) + len <= K);
+      if (live) {
+        gpd_detail *det = P.detail ? P.detail + fi : nullptr;
+        if (all_in)
+          store_out(P, fi, decode_packet<false>(LdsSrc<false>{slot, off & 15u}, len, T, P.first, options, nullptr, det));
+        else
+          store_out(P, fi, decode_packet<false>(HybSrc<K>{P.data, off, gb, slot}, len, T, P.first, options, nullptr, det));
+      }
     }
   }
 }
@@ -2115,7 +2121,7 @@ __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
     cov_d = cov_n;
   }
   if (lane == 0u) P.fb_wcount[gw] = fb_c;  // (gpd_last_launch_split's count)
-  decode_fallback_list<(uint32_t)STAGE / 64u>(P, buf, fb_start, fb_c, lane, dlen, options);
+  decode_fallback_list<(uint32_t)STAGE / 64u, CS, HASH>(P, buf, fb_start, fb_c, lane, dlen, options);
 }
 
 // ---------------------------------------------------------------- round-based header-once loop
@@ -2404,7 +2410,7 @@ __global__ __launch_bounds__(256, MINW) void ro_kernel(KParams P) {
     }
   }
   if (lane == 0u) P.fb_wcount[gw] = fb_c;  // (gpd_last_launch_split's count)
-  decode_fallback_list<kRoStage / 64u>(P, buf, fb_start, fb_c, lane, dlen, options);
+  decode_fallback_list<kRoStage / 64u, CS, HASH>(P, buf, fb_start, fb_c, lane, dlen, options);
 }
 
 template <int STAGE, bool FAST, bool EXT, bool PAGES, bool SWZ, int WAVES, bool CS = true,
