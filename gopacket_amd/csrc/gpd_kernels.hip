@@ -1758,19 +1758,34 @@ __device__ __forceinline__ void decode_fallback_list(const KParams &P, uint32_t 
     // readable bound of the batch contract (gpd.h gpd_batch: round_up(data_len, 16)): every
     // 16-byte chunk below it is whole, so no staging load reaches past it
     const uint64_t rlim = ((uint64_t)dlen + 15u) & ~15ull;
-    for (uint32_t j = lane; j - lane < fb_c; j += 64u) {
-      const bool live = j < fb_c;
-      const uint32_t fi = live ? P.fb_list[fb_start + j] : 0u;
-      const uint32_t off = live ? min(P.offset[fi], dlen) : 0u;
-      const uint32_t len = live ? min(P.caplen[fi], dlen - off) : 0u;
-      const uint64_t gb = (uint64_t)off & ~15ull;
+    // round j's descriptors and first K bytes; the next round's are fetched before this round
+    // decodes (registers are free at the wave's end), so their three dependent global loads
+    // (list entry, descriptor, bytes) overlap the decode instead of preceding it
+    struct Fetch {
+      uint32_t fi, off, len;
       v4u32 c[K / 16u];
+    };
+    auto fetch = [&](uint32_t j, Fetch &f) {
+      const bool live = j < fb_c;
+      f.fi = live ? P.fb_list[fb_start + j] : 0u;
+      f.off = live ? min(P.offset[f.fi], dlen) : 0u;
+      f.len = live ? min(P.caplen[f.fi], dlen - f.off) : 0u;
+      const uint64_t gb = (uint64_t)f.off & ~15ull;
 #pragma unroll
       for (uint32_t k = 0; k < K / 16u; k++)
-        c[k] = (live && gb + 16u * k < rlim) ? *reinterpret_cast<const v4u32 *>(P.data + gb + 16u * k)
-                                              : v4u32{0u, 0u, 0u, 0u};
+        f.c[k] = (live && gb + 16u * k < rlim) ? *reinterpret_cast<const v4u32 *>(P.data + gb + 16u * k)
+                                                : v4u32{0u, 0u, 0u, 0u};
+    };
+    Fetch cur;
+    fetch(lane, cur);
+    for (uint32_t j = lane; j - lane < fb_c; j += 64u) {
+      const bool live = j < fb_c;
 #pragma unroll
-      for (uint32_t k = 0; k < K / 16u; k++) *reinterpret_cast<v4u32 *>(g_lds + slot + 16u * k) = c[k];
+      for (uint32_t k = 0; k < K / 16u; k++) *reinterpret_cast<v4u32 *>(g_lds + slot + 16u * k) = cur.c[k];
+      Fetch nxt;
+      if (j + 64u - lane < fb_c) fetch(j + 64u, nxt);  // (wave-uniform)
+      const uint32_t fi = cur.fi, off = cur.off, len = cur.len;
+      const uint64_t gb = (uint64_t)off & ~15ull;
       // a round whose packets all lie inside their slots reads LDS only (no per-read bound)
       const bool all_in = __all(!live || (off & 15u) + len <= K);
       if (live) {
@@ -1780,6 +1795,7 @@ __device__ __forceinline__ void decode_fallback_list(const KParams &P, uint32_t 
         else
           store_out(P, fi, decode_packet<false>(HybSrc<K>{P.data, off, gb, slot}, len, T, P.first, options, nullptr, det));
       }
+      cur = nxt;
     }
   }
 }
