@@ -263,23 +263,44 @@ __device__ __forceinline__ uint16_t fold_not(uint32_t csum) {
 constexpr uint64_t kFnvBasis = 14695981039346656037ULL;  // flows.go:69
 constexpr uint64_t kFnvPrime = 1099511628211ULL;         // flows.go:70
 
-// FNV-1a over the low `nbytes` bytes of little-endian word w, flows.go:60-67.
-// h * prime = h * 0x1b3 + (h << 40) (fnvPrime = 2^40 + 0x1b3).
-__device__ __forceinline__ uint64_t fnv_word(uint64_t h, uint32_t w, int nbytes) {
+// FNV-1a (flows.go:60-67) with fnvPrime = 2^40 + 0x1b3: h * prime = h * 0x1b3 + (h << 40), the
+// 64-bit state as two words (one 32x32->64 multiply per byte).
+struct H64 {
+  uint32_t lo, hi;
+};
+__device__ __forceinline__ H64 fnv_mulp(H64 h) {
+  const uint64_t p = (uint64_t)h.lo * 0x1b3u;
+  return H64{(uint32_t)p, h.hi * 0x1b3u + (uint32_t)(p >> 32) + (h.lo << 8)};
+}
+constexpr uint64_t kFnvC0 = (kFnvBasis & ~0xFFull) * kFnvPrime;  // (basis with byte 0 cleared) * prime
+// fnvHash of the NB low bytes of w (byte 0 first), from the basis
+template <int NB>
+__device__ __forceinline__ H64 fnv_start(uint32_t w) {
+  static_assert(NB == 2 || NB == 4, "fnv_start<2|4>");
+  // byte 0 in closed form: (basis ^ b) * prime = C0 + c * 0x1b3 + (c << 40), c = b ^ 0x25
+  const uint32_t c = (w & 0xFFu) ^ (uint32_t)(kFnvBasis & 0xFFu);
+  const uint64_t r = (uint64_t)c * 0x1b3u + kFnvC0;
+  H64 x{(uint32_t)r, (uint32_t)(r >> 32) + (c << 8)};
+#pragma unroll
+  for (int j = 1; j < NB; j++) {
+    x.lo ^= (w >> (8 * j)) & 0xFFu;
+    x = fnv_mulp(x);
+  }
+  return x;
+}
+__device__ __forceinline__ H64 fnv_more(H64 x, uint32_t w) {  // four more bytes
 #pragma unroll
   for (int j = 0; j < 4; j++) {
-    if (j < nbytes) {
-      h ^= (uint64_t)((w >> (8 * j)) & 0xFFu);
-      h = h * 0x1b3ull + (h << 40);
-    }
+    x.lo ^= (w >> (8 * j)) & 0xFFu;
+    x = fnv_mulp(x);
   }
-  return h;
+  return x;
 }
 // Flow.FastHash, flows.go:167-174
-__device__ __forceinline__ uint64_t flow_mix(uint64_t hs, uint64_t hd, uint32_t ept) {
-  uint64_t h = hs + hd;
-  h ^= (uint64_t)ept;
-  return h * kFnvPrime;
+__device__ __forceinline__ uint64_t flow_fast(H64 s, H64 d, uint32_t ept) {
+  const uint64_t sum = (((uint64_t)s.hi << 32) | s.lo) + (((uint64_t)d.hi << 32) | d.lo);
+  const H64 x = fnv_mulp(H64{(uint32_t)sum ^ ept, (uint32_t)(sum >> 32)});
+  return ((uint64_t)x.hi << 32) | x.lo;
 }
 
 // ---------------------------------------------------------------- one packet
@@ -621,22 +642,21 @@ done:
   if (last_net == 1 || (last_tp && tp_net == 1)) load_words(s, ip4_off + 12, v4);
   if (!(options & GPD_OPT_NO_FLOW_HASH)) {
     if (last_net == 1) {  // ip4.NetworkFlow(), ip4.go:63-65
-      nhash = flow_mix(fnv_word(kFnvBasis, v4[0], 4), fnv_word(kFnvBasis, v4[1], 4), 1u);
+      nhash = flow_fast(fnv_start<4>(v4[0]), fnv_start<4>(v4[1]), 1u);
       st |= 1u << 16;
     } else if (last_net == 2) {  // ip6.NetworkFlow(), ip6.go:49-51
       uint32_t w[8];
       load_words(s, ip6_off + 8, w);
-      uint64_t hs = kFnvBasis, hd = kFnvBasis;
-#pragma unroll
-      for (int k = 0; k < 4; k++) { hs = fnv_word(hs, w[k], 4); hd = fnv_word(hd, w[k + 4], 4); }
-      nhash = flow_mix(hs, hd, 2);
+      const H64 hs = fnv_more(fnv_more(fnv_more(fnv_start<4>(w[0]), w[1]), w[2]), w[3]);
+      const H64 hd = fnv_more(fnv_more(fnv_more(fnv_start<4>(w[4]), w[5]), w[6]), w[7]);
+      nhash = flow_fast(hs, hd, 2u);
       st |= 1u << 16;
     }
     if (last_tp) {  // tcp/udp.TransportFlow(), tcp.go:331-333, udp.go:123-125
       uint32_t w[1];
       load_words(s, last_tp == 1 ? tcp_poff : udp_off, w);
       uint32_t ept = last_tp == 1 ? 4u : 5u;
-      thash = flow_mix(fnv_word(kFnvBasis, w[0], 2), fnv_word(kFnvBasis, w[0] >> 16, 2), ept);
+      thash = flow_fast(fnv_start<2>(w[0]), fnv_start<2>(w[0] >> 16), ept);
       st |= 1u << 17;
     }
   }
@@ -764,44 +784,6 @@ __device__ __forceinline__ uint32_t fold_le_not(uint32_t s) {
 
 // FNV-1a (flows.go:60-67) on (lo, hi) halves.  h * fnvPrime with fnvPrime = 2^40 + 0x1b3:
 // lo' = lo * 0x1b3, hi' = hi * 0x1b3 + carry + (lo << 8) (mod 2^32).
-struct H64 {
-  uint32_t lo, hi;
-};
-__device__ __forceinline__ H64 fnv_mulp(H64 h) {
-  const uint64_t p = (uint64_t)h.lo * 0x1b3u;
-  return H64{(uint32_t)p, h.hi * 0x1b3u + (uint32_t)(p >> 32) + (h.lo << 8)};
-}
-constexpr uint64_t kFnvC0 = (kFnvBasis & ~0xFFull) * kFnvPrime;  // (basis with byte 0 cleared) * prime
-// fnvHash of the NB low bytes of w (byte 0 first), from the basis
-template <int NB>
-__device__ __forceinline__ H64 fnv_start(uint32_t w) {
-  static_assert(NB == 2 || NB == 4, "fnv_start<2|4>");
-  // byte 0 in closed form: (basis ^ b) * prime = C0 + c * 0x1b3 + (c << 40), c = b ^ 0x25
-  const uint32_t c = (w & 0xFFu) ^ (uint32_t)(kFnvBasis & 0xFFu);
-  const uint64_t r = (uint64_t)c * 0x1b3u + kFnvC0;
-  H64 x{(uint32_t)r, (uint32_t)(r >> 32) + (c << 8)};
-#pragma unroll
-  for (int j = 1; j < NB; j++) {
-    x.lo ^= (w >> (8 * j)) & 0xFFu;
-    x = fnv_mulp(x);
-  }
-  return x;
-}
-__device__ __forceinline__ H64 fnv_more(H64 x, uint32_t w) {  // four more bytes
-#pragma unroll
-  for (int j = 0; j < 4; j++) {
-    x.lo ^= (w >> (8 * j)) & 0xFFu;
-    x = fnv_mulp(x);
-  }
-  return x;
-}
-// Flow.FastHash, flows.go:167-174
-__device__ __forceinline__ uint64_t flow_fast(H64 s, H64 d, uint32_t ept) {
-  const uint64_t sum = (((uint64_t)s.hi << 32) | s.lo) + (((uint64_t)d.hi << 32) | d.lo);
-  const H64 x = fnv_mulp(H64{(uint32_t)sum ^ ept, (uint32_t)(sum >> 32)});
-  return ((uint64_t)x.hi << 32) | x.lo;
-}
-
 struct FastCtx {        // wave-uniform facts about the registered set and the options
   uint32_t mult;        // the fixed-layout hash multiplier
   uint32_t pl_raw;      // Payload as a raw slot: LayerType 2 << 8 | its LUT entry
