@@ -127,6 +127,26 @@ def test_error_sites_detail_and_texts():
         assert_same(host, ref, b, ext=False)
 
 
+def test_error_sites_detail_round_kernel():
+    """The error sites and deep stacks among IMIX frames, through the round kernel
+    (header_once 2: its waves' fallback rounds write the detail records) and the windowed
+    kernels: detail and the texts rebuilt from it equal the oracle's."""
+    import error_sites as ES
+    bulk = synth.make_imix(4096, seed=0x5EED0631)
+    pk = [bulk.packet(i) for i in range(bulk.n)]
+    for k, p in enumerate(ES.packets()):
+        pk.insert(29 * k + 3, p)
+    b = PacketBatch.from_packets(pk)
+    ref = O.decode(b, L.LayerTypeEthernet, ALL, 0, ext=True, nthreads=8)
+    for ho in (2, 1, 0):
+        p = _parser()
+        p.Tuning = dict(header_once=ho)
+        dev = p.DecodeBatch(b, ext=False)
+        assert dev.detail is not None
+        assert_same(dev, ref, b, ext=False)
+        assert_detail(dev, ref)
+
+
 META = G.load()
 CASES = META["cases"]
 
