@@ -1092,7 +1092,32 @@ __device__ __forceinline__ bool fast_decode(uint32_t p, uint32_t len, const Fast
       load64(W, p + b + 14);
     }
     const uint32_t et0 = be_lo(e.y), et1 = be_lo(e.z), et2 = be_lo(e.w);
-    if (et0 < 0x0600u) return false;  // 802.3 length framing (LLC): the generic decoder
+    if (et0 < 0x0600u) {  // 802.3 length framing
+      // header-once tile decode only (the per-window kernels leave it to the generic decoder):
+      // Ethernet's payload is Length bytes (ethernet.go:53-58), then LLC (llc.go:31-52) from the
+      // staged bytes 14..16, then its next layer (llc.go:61-69) — which must stop the decode
+      if (!HO || b != 0u) return false;
+      const uint32_t re = fix_bucket<kFixEthBase>(F.mult, 0u);  // EthernetTypeLLC
+      if ((re & 15u) != D_LLC) return false;
+      uint32_t pl = lim - 14u;
+      if (pl < et0) trunc = 1;
+      else pl = et0;
+      if (pl < 3u) return false;  // "LLC header too small": the generic decoder
+      const uint32_t dsap = (e.y >> 16) & 0xFEu, ssap = (e.y >> 24) & 0xFEu, ctl = e.z & 0xFFu;
+      uint32_t cl = 3;
+      if (!(ctl & 1u) || (ctl & 3u) == 1u) {  // two-byte control field
+        if (pl < 4u) return false;
+        cl = 4;
+      }
+      put(GPD_C_ETHERNET);
+      put((re >> 4) & 15u);
+      if (pl == cl) break;  // layers_decoder.go:71-73
+      const uint32_t nt = (dsap == 0xAAu && ssap == 0xAAu) ? (uint32_t)GPD_LT_SNAP
+                        : (dsap == 0x42u && ssap == 0x42u) ? (uint32_t)GPD_LT_STP : (uint32_t)GPD_LT_ZERO;
+      if ((reinterpret_cast<const uint8_t *>(g_lds)[nt] & 15u) != D_NONE) return false;
+      stop = nt;
+      break;
+    }
     const uint32_t t1 = tag_type(et0), t2 = t1 & tag_type(et1);
     const uint32_t l3 = b + 14 + 4 * (t1 + t2);
     if (t1 && !HO) load64(W, p + l3);  // tagged: the network header is further in
