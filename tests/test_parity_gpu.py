@@ -703,10 +703,10 @@ def test_traffic_mix_both_kernels(mask):
 
 def test_fallback_split_counts_the_generic_share():
     """gpd_last_launch_split: the fast decode takes ICMPv4, IPv6/TCP and VXLAN itself, and
-    leaves exactly the IPv4-options, fragment, hop-by-hop, LLC and cut-TCP frames to the generic
-    decoder (each wave's fallback list, decoded at the end of that wave) — with header-once off.
-    With header-once on (the mix's long frames choose it), a wave's few VXLAN frames fall back
-    too, and the results stay exact."""
+    (and IPv4 fragments) itself, and leaves exactly the IPv4-options, hop-by-hop, LLC/STP and
+    cut-TCP frames to the generic decoder (each wave's fallback list, decoded at the end of that
+    wave) — with header-once off.  With header-once on (the mix's long frames choose it), a
+    wave's few VXLAN frames fall back too, and the results stay exact."""
     import ctypes as C
     from gopacket_amd import parser as P
     from gopacket_amd._lib import check, lib
