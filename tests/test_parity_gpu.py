@@ -101,7 +101,6 @@ def run_both(batch, first=L.LayerTypeEthernet, mask=ALL, options=0, tables=None,
         assert_same(dev, ref, batch, e)
         out = out or dev
     return out  # the ext result when ext records were asked for
-    return dev
 
 
 def test_error_sites_detail_and_texts():
@@ -855,6 +854,43 @@ def test_long_frame_mutations_both_ways(ho):
         if rng.random() < 0.1 and lens[i] >= 70:  # NOP NOP Timestamps on a 32-B TCP header
             data[o + 18 + 20 + 12] = 0x80
             data[o + 58:o + 62] = (1, 1, 8, 10)
+    b = PacketBatch(data, base.data_len, base.offset.copy(), lens.astype(np.uint32))
+    t = dict(window_bytes=8192, header_once=ho)
+    run_both(b, ext=False, tuning=t)
+    run_both(b, L.LayerTypeEthernet, 0x3FF, ext=False, tuning=t)
+
+
+@pytest.mark.parametrize("ho", [0, 1, 2])
+def test_llc_frames_in_every_kernel(ho):
+    """802.3 length framing among long frames: Length below, at and above the captured payload,
+    0..4 bytes of LLC, SNAP / STP / other SAP pairs, one- and two-byte control fields
+    (ethernet.go:53-58, llc.go:31-69) — the header-once tile decode takes these frames itself
+    (gpd_kernels.hip fast_decode<HO>, the et0 < 0x0600 exit), the windowed kernels leave them to
+    the generic decoder; with LLC registered and not, against the oracle."""
+    rng = np.random.default_rng(77 + ho)
+    base = synth.make_imix(1 << 12)
+    n = base.n
+    data = base.data.copy()
+    offs, lens = base.offset.astype(np.int64), base.caplen.astype(np.int64).copy()
+    saps = ((0xAA, 0xAA), (0x42, 0x42), (0xAB, 0xAA), (0x43, 0x43), (0xF0, 0xF0), (0x06, 0x07))
+    for i in rng.choice(n, size=n // 3, replace=False):
+        o = int(offs[i])
+        pl = int(lens[i]) - 14
+        r = rng.random()
+        if r < 0.3:
+            ln = pl  # Length = the payload
+        elif r < 0.5:
+            ln = int(rng.integers(0, 5))  # 0..4 bytes of LLC
+        elif r < 0.75:
+            ln = int(rng.integers(0, max(pl, 1)))  # Ethernet padding trimmed
+        else:
+            ln = int(rng.integers(pl, 0x600))  # longer than captured: truncated
+        ln = min(ln, 0x5FF)
+        data[o + 12:o + 14] = (ln >> 8, ln & 0xFF)
+        d, sp = saps[int(rng.integers(0, len(saps)))]
+        data[o + 14:o + 17] = (d, sp, int(rng.choice([0x03, 0x00, 0x01, 0xF3, 0x02, 0x05])))
+        if rng.random() < 0.15:
+            lens[i] = int(rng.integers(12, min(lens[i], 40) + 1))  # cut inside the LLC header
     b = PacketBatch(data, base.data_len, base.offset.copy(), lens.astype(np.uint32))
     t = dict(window_bytes=8192, header_once=ho)
     run_both(b, ext=False, tuning=t)
