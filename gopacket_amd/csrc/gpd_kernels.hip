@@ -1950,7 +1950,7 @@ __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
   };
   // Shifted copies pay for themselves where windows hold many small frames; the host sets
   // the bit from the batch's mean slot (measured: tools/ab_shift.sh).
-  const bool noshift = (P.options & kShiftWindows) == 0;
+  const bool noshift = AL || (P.options & kShiftWindows) == 0;  // (AL: launched for unshifted windows only)
   auto wshift = [&](const Window &w) -> uint32_t { return noshift ? 0u : w.shift; };
   // COOP: the chunk prefix sums of a window are computed from the registers as it is
   // committed when the wave's previous window needed them (`pfx_pred`); otherwise, if this
@@ -2082,7 +2082,7 @@ __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
         }
       }
     }
-    {  // learn where this wave's network headers sit (mod 16) for the next windows' shift
+    if constexpr (!AL) {  // learn where this wave's network headers sit (mod 16) for the next windows' shift
       const uint32_t no = res.hoff & 0xFFFFu;
       const uint64_t hm = __ballot(cov_d && no != 0xFFFFu);
       if (hm) l3m = (uint32_t)__builtin_amdgcn_readlane((int)no, (int)__builtin_ctzll(hm)) & 15u;
