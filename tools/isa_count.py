@@ -17,8 +17,8 @@ subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++
                 "--cuda-device-only", src, "-o", out], check=True, capture_output=True)
 txt = open(out).read()
 want = {"4096 CS HASH w4": "rs_kernelILi4096ELb1ELb1ELi4ELb0ELb1ELb0E",
-        "8192 AL": "rs_kernelILi8192ELb1ELb1ELi3ELb0ELb0ELb0ELb1E",
-        "8192 plain": "rs_kernelILi8192ELb1ELb1ELi3ELb0ELb0ELb0ELb0E",
+        "8192 AL": "rs_kernelILi8192ELb1ELb1ELi3ELb0ELb0ELb0ELb1ELb0E",
+        "8192 plain": "rs_kernelILi8192ELb1ELb1ELi3ELb0ELb0ELb0ELb0ELb0E",
         "8192 HO": "rs_kernelILi8192ELb1ELb1ELi3ELb0ELb1ELb1E"}
 for label, key in want.items():
     m = re.search(r"\n(_ZN3gpd9" + key + r"\S*):", txt)
