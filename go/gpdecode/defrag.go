@@ -105,12 +105,17 @@ func (p *BatchDecodingLayerParser) FragmentsFrom(b *PacketBatch, r *Result) ([]F
 
 func (p *BatchDecodingLayerParser) fragments(b *PacketBatch, r *Result) ([]Fragment, error) {
 	n := len(b.Offset)
-	if n == 0 {
+	if n == 0 || len(b.Data) == 0 { // no packet bytes: no packet can be an IPv4 fragment
 		return nil, nil
 	}
 	if err := p.configure(); err != nil {
 		return nil, err
 	}
+	done, err := p.onDevice()
+	if err != nil {
+		return nil, err
+	}
+	defer done()
 	sizes := []int{(len(b.Data)+15)&^15 + 64, 4 * n, 4 * n, 4 * n, 8 * n, 4 * n, 32 * n}
 	bufs := make([]devBuf, len(sizes))
 	for k, s := range sizes {

@@ -82,13 +82,18 @@ func decoderBit(d gopacket.DecodingLayer) (uint32, error) {
 }
 
 // BatchDecodingLayerParser is the batch form of gopacket.DecodingLayerParser.
+// IgnoreUnsupported and IgnorePanic are plain fields, as in the reference
+// (parser.go:182-195,336-350): assigning one changes the next call's options in
+// place (gpd_ctx_set_options), and the context keeps its device, decoders and the
+// tables ReloadTables gave it.
 type BatchDecodingLayerParser struct {
 	ctx               *C.gpd_ctx
+	device            int
 	first             gopacket.LayerType
 	decoders          uint32
 	IgnoreUnsupported bool // parser.go:336-350
 	IgnorePanic       bool
-	options           uint32
+	options           uint32 // the options the context holds
 }
 
 // NewBatchDecodingLayerParser mirrors gopacket.NewDecodingLayerParser
@@ -96,7 +101,7 @@ type BatchDecodingLayerParser struct {
 // IPProtocolMetadata, the TCP/UDP port maps) are snapshotted when the device
 // context is created; call ReloadTables after layers.Register*PortLayerType.
 func NewBatchDecodingLayerParser(device int, first gopacket.LayerType, decoders ...gopacket.DecodingLayer) (*BatchDecodingLayerParser, error) {
-	p := &BatchDecodingLayerParser{first: first}
+	p := &BatchDecodingLayerParser{device: device, first: first}
 	for _, d := range decoders {
 		bit, err := decoderBit(d)
 		if err != nil {
@@ -111,6 +116,24 @@ func NewBatchDecodingLayerParser(device int, first gopacket.LayerType, decoders 
 	runtime.SetFinalizer(p, (*BatchDecodingLayerParser).Close)
 	return p, nil
 }
+
+// AddDecodingLayer mirrors (*DecodingLayerParser).AddDecodingLayer (parser.go:197-202):
+// the decoder joins the registered set of the existing context (gpd_ctx_add_decoders),
+// whose device and reloaded tables stay.
+func (p *BatchDecodingLayerParser) AddDecodingLayer(d gopacket.DecodingLayer) error {
+	bit, err := decoderBit(d)
+	if err != nil {
+		return err
+	}
+	if rc := C.gpd_ctx_add_decoders(p.ctx, C.uint32_t(bit)); rc != C.GPD_OK {
+		return lastError("gpd_ctx_add_decoders", rc)
+	}
+	p.decoders |= bit
+	return nil
+}
+
+// Device is the GPU the parser decodes on.
+func (p *BatchDecodingLayerParser) Device() int { return p.device }
 
 // Close releases the device context.
 func (p *BatchDecodingLayerParser) Close() {
@@ -218,11 +241,13 @@ func (p *BatchDecodingLayerParser) DecodeBatch(b *PacketBatch) (*Result, error) 
 	if n == 0 {
 		return r, nil
 	}
-	// the data buffer must be readable to round_up(len, 16) + 16
+	// the data buffer must be readable to round_up(len, 16) + 16; it is never empty here, so
+	// a batch of empty packets (every CapLen 0, len(b.Data) == 0) still passes a valid pointer
 	data := b.Data
 	if cap(data) < len(data)+32 {
 		data = append(make([]byte, 0, len(data)+32), data...)
 	}
+	data = data[:len(data)+1]
 	in := C.gpd_batch{
 		data:     (*C.uint8_t)(unsafe.Pointer(&data[0])),
 		data_len: C.uint64_t(len(b.Data)),
@@ -278,7 +303,8 @@ func pinFirst(pn *runtime.Pinner, slices ...interface{}) {
 	}
 }
 
-// configure re-creates the context when the parser options changed.
+// configure hands changed IgnoreUnsupported / IgnorePanic fields to the context in place
+// (gpd_ctx_set_options, ABI 8): the device, the decoder set and the reloaded tables stay.
 func (p *BatchDecodingLayerParser) configure() error {
 	var o uint32
 	if p.IgnoreUnsupported {
@@ -290,13 +316,10 @@ func (p *BatchDecodingLayerParser) configure() error {
 	if o == p.options {
 		return nil
 	}
-	cfg := C.gpd_config{first_layer: C.uint32_t(p.first), decoders: C.uint32_t(p.decoders), options: C.uint32_t(o)}
-	var ctx *C.gpd_ctx
-	if rc := C.gpd_ctx_create(0, &cfg, &ctx); rc != C.GPD_OK {
-		return lastError("gpd_ctx_create", rc)
+	if rc := C.gpd_ctx_set_options(p.ctx, C.uint32_t(o)); rc != C.GPD_OK {
+		return lastError("gpd_ctx_set_options", rc)
 	}
-	p.Close()
-	p.ctx, p.options = ctx, o
+	p.options = o
 	return nil
 }
 

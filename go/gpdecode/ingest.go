@@ -220,6 +220,26 @@ func (t *FlowTable) Close() {
 
 type devBuf struct{ p unsafe.Pointer }
 
+// onDevice pins the goroutine to its OS thread and makes the parser's GPU current there, so
+// the hipMalloc / hipMemcpy calls that follow land on the context's device (HIP's current
+// device is per thread).  The returned func undoes the pin.
+func (p *BatchDecodingLayerParser) onDevice() (func(), error) {
+	runtime.LockOSThread()
+	if e := C.hipSetDevice(C.int(p.device)); e != C.hipSuccess {
+		runtime.UnlockOSThread()
+		return nil, fmt.Errorf("hipSetDevice(%d): %s", p.device, C.GoString(C.hipGetErrorString(e)))
+	}
+	return runtime.UnlockOSThread, nil
+}
+
+// bytesPtr is &b[0], or nil for an empty slice (a batch of empty packets has no bytes).
+func bytesPtr(b []byte) unsafe.Pointer {
+	if len(b) == 0 {
+		return nil
+	}
+	return unsafe.Pointer(&b[0])
+}
+
 func devAlloc(n int) (devBuf, error) {
 	var p unsafe.Pointer
 	if e := C.hipMalloc(&p, C.size_t(n+16)); e != C.hipSuccess {
@@ -253,6 +273,11 @@ func (t *FlowTable) Insert(b *PacketBatch) (*Result, []uint32, error) {
 	if err := t.parser.configure(); err != nil {
 		return nil, nil, err
 	}
+	done, err := t.parser.onDevice()
+	if err != nil {
+		return nil, nil, err
+	}
+	defer done()
 	sizes := []int{(len(b.Data)+15)&^15 + 64, 4 * n, 4 * n, 4 * n, 8 * n, 8 * n, 8 * n, 4 * n, 4 * n, 4 * n}
 	bufs := make([]devBuf, len(sizes))
 	for k, s := range sizes {
@@ -263,7 +288,7 @@ func (t *FlowTable) Insert(b *PacketBatch) (*Result, []uint32, error) {
 		bufs[k] = d
 		defer d.free()
 	}
-	if err := toDev(bufs[0], unsafe.Pointer(&b.Data[0]), len(b.Data)); err != nil {
+	if err := toDev(bufs[0], bytesPtr(b.Data), len(b.Data)); err != nil {
 		return nil, nil, err
 	}
 	if err := toDev(bufs[1], unsafe.Pointer(&b.Offset[0]), 4*n); err != nil {

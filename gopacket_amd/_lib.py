@@ -11,7 +11,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libgpd.so")
 
-GPD_ABI_VERSION = 7
+GPD_ABI_VERSION = 8
 GPD_OK = 0
 GPD_ERR_INVALID = -1
 
@@ -51,6 +51,8 @@ EXPORTS = {
     "gpd_default_tables": (None, [C.c_void_p] * 4),
     "gpd_ctx_create": (C.c_int, [C.c_int, C.POINTER(GpdConfig), C.POINTER(C.c_void_p)]),
     "gpd_ctx_reload_tables": (C.c_int, [C.c_void_p, C.POINTER(GpdConfig)]),
+    "gpd_ctx_set_options": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "gpd_ctx_add_decoders": (C.c_int, [C.c_void_p, C.c_uint32]),
     "gpd_ctx_destroy": (C.c_int, [C.c_void_p]),
     "gpd_decode": (C.c_int, [C.c_void_p, C.POINTER(GpdBatch), C.POINTER(GpdResult), C.c_void_p]),
     "gpd_decode_host": (C.c_int, [C.c_void_p, C.POINTER(GpdBatch), C.POINTER(GpdResult)]),

@@ -2262,7 +2262,10 @@ __global__ __launch_bounds__(256, MINW) void ro_kernel(KParams P) {
     const uint32_t bytes = __builtin_amdgcn_readfirstlane(wave_sum(valid ? min(end - off, 1u << 24) : 0u));
     t0_p = lo;
     t1_p = hi;
-    nr_p = (hi > lo && (uint64_t)(hi - lo) <= 2ull * bytes + kRoStage) ? (hi - lo + kRoStage - 1u) / kRoStage : 0u;
+    const uint32_t nr = (uint32_t)(((uint64_t)(hi - lo) + kRoStage - 1u) / kRoStage);
+    // (a header's round is kept in 16 bits of the lane state: a run of more than 0xFFFF rounds,
+    // 512 MiB, goes to the fallback list too)
+    nr_p = (hi > lo && (uint64_t)(hi - lo) <= 2ull * bytes + kRoStage && nr <= 0xFFFFu) ? nr : 0u;
   };
   v4u32 wv[NC];
   auto rload = [&](uint32_t base, uint32_t nbytes) {  // one round's bytes into the registers

@@ -203,6 +203,9 @@ struct gpd_ctx {
   uint32_t first = GPD_LT_ETHERNET;
   uint32_t decoders = GPD_DEC_ALL;
   uint32_t options = 0;
+  // the dispatch tables last loaded (LayerType values): AddDecodingLayer rebuilds the LDS image
+  // from them, as the reference's parser reads the live tables at each decode
+  std::vector<uint16_t> t_eth, t_proto, t_tcp, t_udp;
   uint32_t *d_image = nullptr;  // LUT + ipproto (+ hashes)
   uint16_t *d_pages = nullptr;  // PAGES fallback
   uint32_t image_words = 0, use_pages = 0;
@@ -316,14 +319,11 @@ void gpd_default_tables(uint16_t *ethertype, uint16_t *ipproto, uint16_t *tcp_po
   if (udp_port) fill(udp_port, 65536, kUdpDefaults);
 }
 
-int gpd_ctx_reload_tables(gpd_ctx *ctx, const gpd_config *cfg) {
-  if (!ctx || !cfg) return set_err(GPD_ERR_INVALID, "gpd_ctx_reload_tables: null argument");
-  std::vector<uint16_t> eth(65536), proto(256), tcp(65536), udp(65536);
-  gpd_default_tables(eth.data(), proto.data(), tcp.data(), udp.data());
-  if (cfg->ethertype) std::memcpy(eth.data(), cfg->ethertype, 65536 * 2);
-  if (cfg->ipproto) std::memcpy(proto.data(), cfg->ipproto, 256 * 2);
-  if (cfg->tcp_port) std::memcpy(tcp.data(), cfg->tcp_port, 65536 * 2);
-  if (cfg->udp_port) std::memcpy(udp.data(), cfg->udp_port, 65536 * 2);
+// The LDS image (and the PAGES blob when the tables do not hash) from ctx's decoder mask and
+// its table snapshot.
+static int build_image(gpd_ctx *ctx) {
+  const std::vector<uint16_t> &eth = ctx->t_eth, &proto = ctx->t_proto, &tcp = ctx->t_tcp,
+                              &udp = ctx->t_udp;
   // LDS image: LUT (32 words) + ipproto with LUT entries (256 words) + the three hashes
   std::vector<uint32_t> img(gpd::kHashLutWords + gpd::kHashProtoWords, 0);
   uint8_t *lut = reinterpret_cast<uint8_t *>(img.data());
@@ -373,6 +373,44 @@ int gpd_ctx_reload_tables(gpd_ctx *ctx, const gpd_config *cfg) {
   return GPD_OK;
 }
 
+int gpd_ctx_reload_tables(gpd_ctx *ctx, const gpd_config *cfg) {
+  if (!ctx || !cfg) return set_err(GPD_ERR_INVALID, "gpd_ctx_reload_tables: null argument");
+  ctx->t_eth.assign(65536, 0);
+  ctx->t_proto.assign(256, 0);
+  ctx->t_tcp.assign(65536, 0);
+  ctx->t_udp.assign(65536, 0);
+  gpd_default_tables(ctx->t_eth.data(), ctx->t_proto.data(), ctx->t_tcp.data(), ctx->t_udp.data());
+  if (cfg->ethertype) std::memcpy(ctx->t_eth.data(), cfg->ethertype, 65536 * 2);
+  if (cfg->ipproto) std::memcpy(ctx->t_proto.data(), cfg->ipproto, 256 * 2);
+  if (cfg->tcp_port) std::memcpy(ctx->t_tcp.data(), cfg->tcp_port, 65536 * 2);
+  if (cfg->udp_port) std::memcpy(ctx->t_udp.data(), cfg->udp_port, 65536 * 2);
+  return build_image(ctx);
+}
+
+// Options the caller may set: the reference's two fields, the engine knobs and the two
+// diagnostic bits bench.py uses (bits 24-29 are the runtime's own launch flags).
+static constexpr uint32_t kUserOptions = GPD_OPT_IGNORE_UNSUPPORTED | GPD_OPT_IGNORE_PANIC |
+                                         GPD_OPT_NO_CHECKSUMS | GPD_OPT_NO_FLOW_HASH |
+                                         (1u << 30) | (1u << 31);
+
+int gpd_ctx_set_options(gpd_ctx *ctx, uint32_t options) {
+  if (!ctx) return set_err(GPD_ERR_INVALID, "gpd_ctx_set_options: ctx is NULL");
+  if (options & ~kUserOptions)
+    return set_err(GPD_ERR_INVALID, "gpd_ctx_set_options: unknown option bits 0x%x",
+                   options & ~kUserOptions);
+  ctx->options = options;
+  return GPD_OK;
+}
+
+int gpd_ctx_add_decoders(gpd_ctx *ctx, uint32_t decoders) {
+  if (!ctx) return set_err(GPD_ERR_INVALID, "gpd_ctx_add_decoders: ctx is NULL");
+  if (decoders & ~GPD_DEC_ALL)
+    return set_err(GPD_ERR_INVALID, "gpd_ctx_add_decoders: unknown decoder bits 0x%x", decoders);
+  if ((ctx->decoders | decoders) == ctx->decoders) return GPD_OK;
+  ctx->decoders |= decoders;
+  return build_image(ctx);
+}
+
 int gpd_ctx_create(int device, const gpd_config *cfg, gpd_ctx **out) {
   if (!out) return set_err(GPD_ERR_INVALID, "gpd_ctx_create: out is NULL");
   *out = nullptr;
@@ -393,6 +431,11 @@ int gpd_ctx_create(int device, const gpd_config *cfg, gpd_ctx **out) {
   ctx->device = device;
   ctx->first = cfg->first_layer;
   ctx->decoders = cfg->decoders;
+  if (cfg->options & ~kUserOptions) {
+    delete ctx;
+    return set_err(GPD_ERR_INVALID, "gpd_ctx_create: unknown option bits 0x%x",
+                   cfg->options & ~kUserOptions);
+  }
   ctx->options = cfg->options;
   hipDeviceProp_t prop;
   if (hipSetDevice(device) != hipSuccess || hipGetDeviceProperties(&prop, device) != hipSuccess) {
@@ -1223,13 +1266,17 @@ static int decode_pcap_host_walk(gpd_ctx *ctx, const uint8_t *buf, uint64_t len,
 // the end, a speculation the walk missed), UINT64_MAX when the call is complete.
 static int decode_device_walk(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, const gpd_pcap_info &I,
                                    uint64_t pos, uint64_t max_n, const gpd_result *out, int nthreads,
-                                   uint64_t *handled, uint64_t *resume, uint64_t *next_pos, int *stop) {
+                                   uint64_t *handled, uint64_t *resume, uint64_t *next_pos, int *stop,
+                                   bool *ineligible) {
   constexpr uint64_t kChunk = (uint64_t)gpd::kPwSeg * gpd::kPwMaxSeg;
   const uint64_t margin = (16ull + I.snaplen + 31ull) & ~15ull;  // the longest record past a chunk
   const uint64_t cap_pkts = kChunk / GPD_PCAP_RECORD_BYTES;       // records a chunk can hold
   *handled = 0;
   *resume = pos;
-  if (I.snaplen > (16u << 20)) return GPD_OK;  // (records that long: the host walk)
+  // (records that long, or a capture whose first records cannot be indexed: the host walk,
+  // for the rest of the call — *ineligible)
+  *ineligible = true;
+  if (I.snaplen > (16u << 20)) return GPD_OK;
   // the mean record size (the decode's staging choices): the first records, walked here
   uint64_t mean = 96;
   {
@@ -1242,6 +1289,7 @@ static int decode_device_walk(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, co
     if (gpd::pcap_index_flat(buf, len, I, pos, 64, 1, o, R) != GPD_OK || R.n == 0) return GPD_OK;
     mean = std::max<uint64_t>(16, (R.next_pos - pos) / R.n);
   }
+  *ineligible = false;
   int rc = alloc_slots(ctx, std::max<uint64_t>(ctx->slot_bytes, kChunk + margin + 64),
                        std::max<uint64_t>(ctx->slot_pkts, cap_pkts), false, out->detail != nullptr);
   if (rc) return rc;
@@ -1396,11 +1444,7 @@ int gpd_decode_pcap_at(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, const gpd
   if (out->records) return set_err(GPD_ERR_INVALID, "gpd_decode_pcap: results as SoA arrays only");
   if (pos > len) return set_err(GPD_ERR_INVALID, "gpd_decode_pcap_at: pos beyond the buffer");
   if (nthreads <= 0) nthreads = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
-  *n_out = 0;
-  if (next_pos) *next_pos = pos;
-  if (stop) *stop = GPD_PCAP_STOP_LIMIT;
-  if (max_n == 0) return GPD_OK;
-  HIP_TRY(hipSetDevice(ctx->device));
+  // this call's diagnostics (gpd_decode_pcap_last_*), reset before any early return
   const double t_call = now_ms();
   g_pt_walk = g_pt_walkwait = g_pt_stage = g_pt_sync = g_pt_drain = 0;
   for (auto &c : g_pw_counts) c = 0;
@@ -1409,7 +1453,12 @@ int gpd_decode_pcap_at(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, const gpd
     double t;
     ~Total() { g_pt_total = now_ms() - t; }
   } total{t_call};
-  const bool dw = ctx->tune.device_walk != 0;
+  *n_out = 0;
+  if (next_pos) *next_pos = pos;
+  if (stop) *stop = GPD_PCAP_STOP_LIMIT;
+  if (max_n == 0) return GPD_OK;
+  HIP_TRY(hipSetDevice(ctx->device));
+  bool dw = ctx->tune.device_walk != 0;
   uint64_t done = 0, at = pos;
   auto shifted = [&](uint64_t d) {
     gpd_result r = *out;
@@ -1426,14 +1475,16 @@ int gpd_decode_pcap_at(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, const gpd
   for (;;) {
     if (dw) {
       uint64_t resume, handled = 0;
+      bool ineligible = false;
       const gpd_result r = shifted(done);
       const int rc = decode_device_walk(ctx, buf, len, *info, at, max_n - done, &r, nthreads, &handled,
-                                        &resume, next_pos, stop);
+                                        &resume, next_pos, stop, &ineligible);
       done += handled;
       *n_out = done;
       if (rc) return rc;
       if (resume == UINT64_MAX) return GPD_OK;
       at = resume;
+      if (ineligible) dw = false;  // one unbounded (pipelined) host walk does the rest
     }
     // The host walk from `at`: all of the call without the device walk; else only the chunk
     // the device walk could not vouch for (a record the reference rejects, a capture ending
@@ -1489,11 +1540,12 @@ constexpr uint64_t kTwTab = kTwMaxBlocks * sizeof(gpd::TwBlock), kTwSt = kTwMaxB
 // A group's per-packet arrays packed into one region, so one D2H brings them back: decode
 // results, caplen (the walk's, the decode's input), then the capture info, each array
 // 256-byte aligned.  The region is laid out for the group's packet count m.
-enum TwArr { kLayers, kNh, kTh, kStatus, kCsum, kHoff, kDet, kCap, kCiOff, kCiTs, kCiWire, kCiIfx, kCiVlan, kCiTci,
+// The detail records come last: they travel (in a copy of their own) only when asked for.
+enum TwArr { kLayers, kNh, kTh, kStatus, kCsum, kHoff, kCap, kCiOff, kCiTs, kCiWire, kCiIfx, kCiVlan, kCiTci, kDet,
              kTwN };
-constexpr uint64_t kTwW[kTwN] = {8, 8, 8, 4, 4, 4, sizeof(gpd_detail), 4, 8, 8, 4, 4, 4, 4};
+constexpr uint64_t kTwW[kTwN] = {8, 8, 8, 4, 4, 4, 4, 8, 8, 4, 4, 4, 4, sizeof(gpd_detail)};
 struct TwLay {
-  uint64_t off[kTwN + 1];  // off[kCiOff]: the end of the region without capture info
+  uint64_t off[kTwN + 1];  // off[kCiOff]: the end of the results; off[kDet]: of the capture info
   explicit TwLay(uint64_t m) {
     uint64_t o = 0;
     for (int a = 0; a < kTwN; a++) {
@@ -1547,10 +1599,10 @@ int gpd::decode_tpv3_device(gpd_ctx *ctx, const gpd_tpv3_ring &R, const std::vec
   };
   std::vector<Group> grp;
   // the caller's array for each region array (NULL: not asked for)
-  void *dst[kTwN] = {out->layers, out->net_hash, out->tp_hash, out->status, out->csum, out->hdr_off, out->detail,
+  void *dst[kTwN] = {out->layers, out->net_hash, out->tp_hash, out->status, out->csum, out->hdr_off,
                      ci ? pk->caplen : nullptr, ci ? pk->offset : nullptr, ci ? pk->ts_ns : nullptr,
                      ci ? pk->wire_len : nullptr, ci ? pk->ifindex : nullptr, ci ? pk->vlan : nullptr,
-                     ci ? pk->vlan_tci : nullptr};
+                     ci ? pk->vlan_tci : nullptr, out->detail};
   // group k done: every block walked as the host would, then its results copied out
   auto complete = [&](size_t k) -> int {
     HIP_TRY(hipEventSynchronize(ctx->ev_tw[k & 3]));
@@ -1656,8 +1708,11 @@ int gpd::decode_tpv3_device(gpd_ctx *ctx, const gpd_tpv3_ring &R, const std::vec
             HIP_TRY(hipMemcpyAsync(static_cast<uint8_t *>(dst[q]) + G.lo * kTwW[q], dev(q), m * kTwW[q],
                                    hipMemcpyDeviceToHost, s.stream_out));
       } else {
-        HIP_TRY(hipMemcpyAsync(s.h_tw + tw_hreg(G.set), dr, L.off[ci ? kTwN : kCiOff], hipMemcpyDeviceToHost,
+        HIP_TRY(hipMemcpyAsync(s.h_tw + tw_hreg(G.set), dr, L.off[ci ? kDet : kCiOff], hipMemcpyDeviceToHost,
                                s.stream_out));
+        if (out->detail)
+          HIP_TRY(hipMemcpyAsync(s.h_tw + tw_hreg(G.set) + L.off[kDet], dr + L.off[kDet], m * kTwW[kDet],
+                                 hipMemcpyDeviceToHost, s.stream_out));
       }
     }
     HIP_TRY(hipEventRecord(ctx->ev_tw[k & 3], s.stream_out));

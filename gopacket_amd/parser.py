@@ -115,13 +115,16 @@ def _torch():
 
 
 class _Ctx:
+    """One gpd_ctx on a device: its decoder set and options change in place (ABI 8), as the
+    reference parser's do; only a new device or first layer makes a new context."""
+
     def __init__(self, device: int, first: int, mask: int, options: int, tables: L.DispatchTables):
         self.tables = tables.copy()
         cfg = self._cfg(first, mask, options)
         h = C.c_void_p()
         check(lib.gpd_ctx_create(device, C.byref(cfg), C.byref(h)), "gpd_ctx_create")
         self.h = h
-        self.key = (device, first, mask, options)
+        self.device, self.first, self.mask, self.options = device, first, mask, options
 
     def _cfg(self, first, mask, options):
         t = self.tables
@@ -130,8 +133,18 @@ class _Ctx:
 
     def reload(self, tables: L.DispatchTables):
         self.tables = tables.copy()
-        cfg = self._cfg(*self.key[1:])
+        cfg = self._cfg(self.first, self.mask, self.options)
         check(lib.gpd_ctx_reload_tables(self.h, C.byref(cfg)), "gpd_ctx_reload_tables")
+
+    def set_options(self, options: int):
+        if options != self.options:
+            check(lib.gpd_ctx_set_options(self.h, options), "gpd_ctx_set_options")
+            self.options = options
+
+    def add_decoders(self, mask: int):
+        if mask | self.mask != self.mask:
+            check(lib.gpd_ctx_add_decoders(self.h, mask), "gpd_ctx_add_decoders")
+            self.mask |= mask
 
     def __del__(self):
         h = getattr(self, "h", None)
@@ -181,7 +194,9 @@ class DeviceResult:
             self.csum = torch.empty(n, dtype=torch.int32, device=dev)
         self.ext = torch.empty(n * EXT_DTYPE.itemsize, dtype=torch.uint8, device=dev) if ext else None
         self.hdr_off = torch.empty(n, dtype=torch.int32, device=dev) if hdr_off else None
-        self.detail = torch.zeros(n * DETAIL_DTYPE.itemsize, dtype=torch.uint8, device=dev) if detail else None
+        # (the kernel writes a packet's detail only where its status asks for one; to_host copies
+        # back just those rows)
+        self.detail = torch.empty(n * DETAIL_DTYPE.itemsize, dtype=torch.uint8, device=dev) if detail else None
 
     def c_result(self) -> GpdResult:
         p = lambda t: t.data_ptr() if t is not None else None
@@ -192,14 +207,31 @@ class DeviceResult:
         u = lambda t, dt: t.cpu().numpy().view(dt)
         ext = self.ext.cpu().numpy().view(EXT_DTYPE) if self.ext is not None else None
         hoff = u(self.hdr_off, np.uint32) if self.hdr_off is not None else None
-        det = self.detail.cpu().numpy().view(DETAIL_DTYPE) if self.detail is not None else None
         if self.records is not None:
             r = self.records.cpu().numpy().view(RECORD_DTYPE)
-            return BatchResult(r["status"].copy(), r["layers"].copy(), r["net_hash"].copy(),
-                               r["tp_hash"].copy(), r["csum"].copy(), ext, hoff, det)
-        return BatchResult(u(self.status, np.uint32), u(self.layers, np.uint64),
-                           u(self.net_hash, np.uint64), u(self.tp_hash, np.uint64),
-                           u(self.csum, np.uint32), ext, hoff, det)
+            res = BatchResult(r["status"].copy(), r["layers"].copy(), r["net_hash"].copy(),
+                              r["tp_hash"].copy(), r["csum"].copy(), ext, hoff, None)
+        else:
+            res = BatchResult(u(self.status, np.uint32), u(self.layers, np.uint64),
+                              u(self.net_hash, np.uint64), u(self.tp_hash, np.uint64),
+                              u(self.csum, np.uint32), ext, hoff, None)
+        if self.detail is not None:
+            res.detail = self._detail_rows(res.status)
+        return res
+
+    def _detail_rows(self, status: np.ndarray) -> np.ndarray:
+        """The detail records of the packets that have one (decode errors, > 12 layers; gpd.h
+        gpd_detail), gathered on the device so the copy back is 24 B per such packet, not per
+        packet; every other entry is zero."""
+        torch = _torch()
+        st = status.astype(np.uint32)
+        rows = np.nonzero(((st & 3) == 2) | (((st >> 4) & 31) > 12) | (((st >> 3) & 1) == 1))[0]
+        det = np.zeros(self.n, DETAIL_DTYPE)
+        if len(rows):
+            d = self.detail.view(self.n, DETAIL_DTYPE.itemsize)
+            idx = torch.from_numpy(rows.astype(np.int64)).to(d.device)
+            det[rows] = d.index_select(0, idx).cpu().numpy().view(DETAIL_DTYPE).reshape(-1)
+        return det
 
 
 class DecodingLayerParser:
@@ -219,6 +251,7 @@ class DecodingLayerParser:
 
     # --- registration (parser.go:197-241) ---------------------------------------
     def AddDecodingLayer(self, d) -> None:
+        """parser.go:197-202; applied to an existing context in place (gpd_ctx_add_decoders)."""
         self._mask |= decoder_mask([d])
 
     @property
@@ -241,10 +274,16 @@ class DecodingLayerParser:
         return o
 
     def ctx(self) -> _Ctx:
-        key = (self.device, self.first, self._mask, self.options)
-        if self._ctx is None or self._ctx.key != key:
-            self._ctx = _Ctx(self.device, self.first, self._mask, self.options, self._tables)
-            self._ctx.tuned = None
+        """The device context, created once per (device, first layer); options and added
+        decoders apply in place (gpd_ctx_set_options / gpd_ctx_add_decoders), so the table
+        snapshot, tuning and staging survive them as the reference parser's state does."""
+        c = self._ctx
+        if c is None or (c.device, c.first) != (self.device, self.first) or c.mask & ~self._mask:
+            self._ctx = c = _Ctx(self.device, self.first, self._mask, self.options, self._tables)
+            c.tuned = None
+        else:
+            c.add_decoders(self._mask)
+            c.set_options(self.options)
         if self._ctx.tuned != self.Tuning:
             self._apply_tuning()
         return self._ctx
@@ -278,8 +317,10 @@ class DecodingLayerParser:
 
     def DecodeBatch(self, batch: PacketBatch, ext: bool = False, detail: bool = True) -> BatchResult:
         """Decode every packet of a host batch on the GPU (H2D, kernel, D2H).  With detail (the
-        default) res.err(i) carries the reference's exact text and res.decoded(i) any depth,
-        and the batch keeps the fast path; ext adds the layer records (generic path)."""
+        default) res.err(i) carries the reference's exact text and res.decoded(i) any depth; the
+        batch keeps the fast path, and only the failing / deep packets' 24-B records come back
+        (a device gather: no extra transfer for a clean batch).  ext adds the layer records
+        (generic path)."""
         torch = _torch()
         db = DeviceBatch(batch, self.device)
         dr = DeviceResult(batch.n, self.device, ext, detail=detail)
@@ -355,18 +396,21 @@ class DecodingLayerParser:
         return n.value, nxt.value, stop.value, err
 
     def DecodeTPv3(self, ring, max_n: int = 1 << 20, max_blocks: Optional[int] = None,
-                   add_vlan_header: bool = False, nthreads: int = 0, out=None, ci=None):
+                   add_vlan_header: bool = False, nthreads: int = 0, out=None, ci=None,
+                   detail: bool = False):
         """Every packet of the user-owned blocks of a TPACKET_V3 ring (afpacket.TPv3Ring) from
         ring.offset on, decoded on the GPU where it lies (gpd_decode_tpv3).  The blocks are not
         released.  Returns (BatchResult, CaptureInfo, blocks walked).  `out` (a BatchResult with
         hdr_off) and `ci` (a CaptureInfo), both of at least max_n entries, are reused when given
-        — a capture loop keeps them across calls instead of touching fresh pages each time."""
+        — a capture loop keeps them across calls instead of touching fresh pages each time.
+        detail adds the gpd_detail records (exact error texts, deep stacks) to a new `out`."""
         from .afpacket import CaptureInfo
         if ci is None:
             ci = CaptureInfo.alloc(max_n)
         res = out if out is not None else BatchResult(
             np.zeros(max_n, np.uint32), np.zeros(max_n, np.uint64), np.zeros(max_n, np.uint64),
-            np.zeros(max_n, np.uint64), np.zeros(max_n, np.uint32), None, np.zeros(max_n, np.uint32))
+            np.zeros(max_n, np.uint64), np.zeros(max_n, np.uint32), None, np.zeros(max_n, np.uint32),
+            np.zeros(max_n, DETAIL_DTYPE) if detail else None)
         if len(res.status) < max_n or res.hdr_off is None or len(ci.offset) < max_n:
             raise ValueError("DecodeTPv3: out / ci must hold max_n entries (out with hdr_off)")
         r = _c_result(res)

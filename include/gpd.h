@@ -16,6 +16,9 @@
  *   gpd_ctx_reload_tables RegisterTCPPortLayerType / RegisterUDPPortLayerType
  *                           layers/ports.go:78-80,126-128 and writes to
  *                           EthernetTypeMetadata / IPProtocolMetadata (layers/enums.go:288)
+ *   gpd_ctx_set_options   assigning parser.IgnoreUnsupported / IgnorePanic  parser.go:182-195,
+ *                           336-350 (plain fields: the parser, its decoders and the tables stay)
+ *   gpd_ctx_add_decoders  (*DecodingLayerParser).AddDecodingLayer       parser.go:197-202
  *   gpd_decode            (*DecodingLayerParser).DecodeLayers        parser.go:302-316
  *                         (loop: layers_decoder.go:60-79), fused with
  *                         TCP.ComputeChecksum                          layers/tcp.go:193-195,
@@ -46,11 +49,13 @@
 extern "C" {
 #endif
 
-#define GPD_ABI_VERSION 7  /* 2: ICMPv4 + LLC, 12 objects, 224-B ext; 3: gpd_result.hdr_off;
+#define GPD_ABI_VERSION 8  /* 2: ICMPv4 + LLC, 12 objects, 224-B ext; 3: gpd_result.hdr_off;
                               4: gpd_ctx_set_tuning; 5: gpd_tuning.header_once,
                               gpd_tuning.device_walk, gpd_result.records; 6: outputs follow the
                               objects as a failing call leaves them; ext err_obj/err_wrote/err_off;
-                              7: gpd_result.detail (error arguments and deep stacks without ext) */
+                              7: gpd_result.detail (error arguments and deep stacks without ext);
+                              8: gpd_ctx_set_options, gpd_ctx_add_decoders (in place: device,
+                              tables and staging kept) */
 
 /* ---- gopacket LayerType numbers (layertypes.go:14-154, decode.go:105-116) ---- */
 #define GPD_LT_ZERO            0
@@ -356,6 +361,16 @@ void gpd_default_tables(uint16_t *ethertype, uint16_t *ipproto,
                         uint16_t *tcp_port, uint16_t *udp_port);
 int  gpd_ctx_create(int device, const gpd_config *cfg, gpd_ctx **out);
 int  gpd_ctx_reload_tables(gpd_ctx *ctx, const gpd_config *cfg);
+/* ABI 8.  Change the options of ctx in place, as assigning the reference's IgnoreUnsupported /
+ * IgnorePanic fields does (parser.go:182-195,336-350): the context keeps its device, decoder set,
+ * dispatch-table snapshot (gpd_ctx_reload_tables), tuning and staging.  Takes effect on the next
+ * launch; launches already enqueued keep the options they were enqueued with.  GPD_ERR_INVALID
+ * on unknown bits (cfg->options of gpd_ctx_create is checked the same way). */
+int  gpd_ctx_set_options(gpd_ctx *ctx, uint32_t options);
+/* ABI 8.  AddDecodingLayer (parser.go:197-202): add GPD_DEC_* decoders to ctx's registered set.
+ * The dispatch image is rebuilt from the context's current table snapshot (the defaults or the
+ * last gpd_ctx_reload_tables), on its device; synchronous. */
+int  gpd_ctx_add_decoders(gpd_ctx *ctx, uint32_t decoders);
 int  gpd_ctx_destroy(gpd_ctx *ctx);
 /* Asynchronous on `stream` (a hipStream_t; NULL = the null stream).  Device pointers. */
 int  gpd_decode(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, void *stream);

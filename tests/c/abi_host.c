@@ -311,9 +311,85 @@ static int check_fragments(gpd_ctx *ctx, hipStream_t s, const gpd_batch *db, con
   return bad;
 }
 
+/* ABI 8: a context reconfigured in place keeps its tables and device, as the reference parser
+ * keeps the global tables when IgnoreUnsupported is assigned (parser.go:182-195,336-350) and
+ * AddDecodingLayer only adds a decoder (parser.go:197-202).  A UDP port is registered as VXLAN
+ * (layers/ports.go:126-128) and the tables reloaded; VXLAN is added afterwards; then
+ * IgnoreUnsupported is flipped both ways; every step decodes host and device batches against the
+ * oracle on the same mutated tables.  Also: an all-empty batch, and unknown option bits. */
+static int check_reconfig(const gpd_config *base, const uint8_t *data, uint64_t data_len,
+                          const uint32_t *off, const uint32_t *cap, uint64_t n, const gpd_batch *db,
+                          const gpd_result *dr, hipStream_t s, uint16_t vxlan_port, uint64_t *vx_out) {
+  uint16_t *et = malloc(65536 * 2), *ip = malloc(256 * 2), *tp = malloc(65536 * 2),
+           *up = malloc(65536 * 2);
+  gpd_default_tables(et, ip, tp, up);
+  up[vxlan_port] = GPD_LT_VXLAN;
+  gpd_config cfg = *base;
+  cfg.decoders = base->decoders & ~GPD_DEC_VXLAN;
+  gpd_ctx *ctx = NULL;
+  CHECK(gpd_ctx_create(0, &cfg, &ctx));
+  cfg.ethertype = et, cfg.ipproto = ip, cfg.tcp_port = tp, cfg.udp_port = up;
+  CHECK(gpd_ctx_reload_tables(ctx, &cfg));
+  CHECK(gpd_ctx_add_decoders(ctx, base->decoders & GPD_DEC_VXLAN));
+  int bad = 0;
+  if (gpd_ctx_set_options(ctx, 1u << 26) != GPD_ERR_INVALID) {
+    fprintf(stderr, "reconfig: internal option bits accepted\n");
+    bad = 1;
+  }
+  res_t hv = res_alloc(n), dv = res_alloc(n), ov = res_alloc(n);
+  gpd_ext_rec *oext = calloc(n + 1, sizeof(gpd_ext_rec));
+  gpo_tables t = {et, ip, tp, up};
+  const uint32_t opts[3] = {base->options ^ GPD_OPT_IGNORE_UNSUPPORTED, base->options,
+                            base->options ^ GPD_OPT_IGNORE_UNSUPPORTED};
+  uint64_t vx = 0;
+  for (int k = 0; k < 3 && !bad; k++) {
+    CHECK(gpd_ctx_set_options(ctx, opts[k]));
+    gpd_batch hb = {data, data_len, off, cap, n};
+    gpd_result hr = {hv.status, hv.layers, hv.net_hash, hv.tp_hash, hv.csum, NULL, hv.hdr_off, NULL, hv.detail};
+    CHECK(gpd_decode_host(ctx, &hb, &hr));
+    CHECK(gpd_decode(ctx, db, dr, s));
+    CHECK(gpd_sync(ctx, s));
+    HCHECK(hipMemcpy(dv.status, dr->status, 4 * n, hipMemcpyDeviceToHost));
+    HCHECK(hipMemcpy(dv.layers, dr->layers, 8 * n, hipMemcpyDeviceToHost));
+    HCHECK(hipMemcpy(dv.net_hash, dr->net_hash, 8 * n, hipMemcpyDeviceToHost));
+    HCHECK(hipMemcpy(dv.tp_hash, dr->tp_hash, 8 * n, hipMemcpyDeviceToHost));
+    HCHECK(hipMemcpy(dv.csum, dr->csum, 4 * n, hipMemcpyDeviceToHost));
+    HCHECK(hipMemcpy(dv.hdr_off, dr->hdr_off, 4 * n, hipMemcpyDeviceToHost));
+    HCHECK(hipMemcpy(dv.detail, dr->detail, sizeof(gpd_detail) * n, hipMemcpyDeviceToHost));
+    gpo_decode_batch(data, off, cap, n, GPD_LT_ETHERNET, base->decoders, opts[k], &t, ov.status,
+                     ov.layers, ov.net_hash, ov.tp_hash, ov.csum, ov.hdr_off, oext, 8);
+    bad |= res_cmp("reconfig host vs oracle", &hv, &ov, n) | res_cmp("reconfig device vs oracle", &dv, &ov, n);
+    if (!bad) bad |= detail_cmp("reconfig detail", &hv, oext, n) | detail_cmp("reconfig detail", &dv, oext, n);
+  }
+  for (uint64_t i = 0; i < n; i++)  /* packets that reached the registered port's VXLAN decoder */
+    for (uint32_t j = 0; j < GPD_STATUS_NLAYERS(ov.status[i]) && j < GPD_CORE_MAX_LAYERS; j++)
+      if (GPD_LAYERS_CODE(ov.layers[i], j) == GPD_C_VXLAN) { vx++; break; }
+  if (!bad && (base->decoders & GPD_DEC_VXLAN) && vx == 0) {
+    fprintf(stderr, "reconfig: no packet decoded VXLAN on the registered port\n");
+    bad = 1;
+  }
+  /* a batch of empty packets (every CapLen 0, no data) */
+  if (!bad) {
+    const uint64_t m = 7;
+    uint32_t z_off[7] = {0}, z_cap[7] = {0};
+    uint8_t z_data[64] = {0};
+    res_t zv = res_alloc(m), zo = res_alloc(m);
+    gpd_batch zb = {z_data, 0, z_off, z_cap, m};
+    gpd_result zr = {zv.status, zv.layers, zv.net_hash, zv.tp_hash, zv.csum, NULL, zv.hdr_off, NULL, zv.detail};
+    CHECK(gpd_decode_host(ctx, &zb, &zr));
+    gpo_decode_batch(z_data, z_off, z_cap, m, GPD_LT_ETHERNET, base->decoders, opts[2], &t,
+                     zo.status, zo.layers, zo.net_hash, zo.tp_hash, zo.csum, zo.hdr_off, oext, 1);
+    bad |= res_cmp("empty batch vs oracle", &zv, &zo, m);
+  }
+  CHECK(gpd_ctx_destroy(ctx));
+  free(et), free(ip), free(tp), free(up), free(oext);
+  *vx_out = vx;
+  return bad;
+}
+
 int main(int argc, char **argv) {
-  if (argc != 2 && argc != 4) {
-    fprintf(stderr, "usage: %s BATCH_FILE [ERR_OUT PROTO_NAMES]\n", argv[0]);
+  if (argc != 2 && argc != 4 && argc != 5) {
+    fprintf(stderr, "usage: %s BATCH_FILE [ERR_OUT PROTO_NAMES [VXLAN_PORT]]\n", argv[0]);
     return 2;
   }
   FILE *f = fopen(argv[1], "rb");
@@ -438,10 +514,15 @@ int main(int argc, char **argv) {
   uint64_t frags = 0;
   if (!bad && n > 0) bad |= check_fragments(ctx, s, &db, &dr, data, off, cap, ov.status, ov.hdr_off, n, &frags);
 
+  /* 7. in-place reconfiguration on a second context (ABI 8) */
+  uint64_t vx = 0;
+  if (!bad && argc >= 5) bad |= check_reconfig(&cfg, data, data_len, off, cap, n, &db, &dr, s,
+                                               (uint16_t)atoi(argv[4]), &vx);
+
   CHECK(gpd_ctx_destroy(ctx));
   HCHECK(hipStreamDestroy(s));
   if (bad) return 1;
-  printf("abi_host ok %llu %llu %llu\n", (unsigned long long)n, (unsigned long long)flows,
-         (unsigned long long)frags);
+  printf("abi_host ok %llu %llu %llu %llu\n", (unsigned long long)n, (unsigned long long)flows,
+         (unsigned long long)frags, (unsigned long long)vx);
   return 0;
 }

@@ -27,6 +27,7 @@ def test_header_declares_the_boundary():
     fns = declared_functions()
     for f in ("gpd_ctx_create", "gpd_decode", "gpd_decode_host", "gpd_sync", "gpd_ctx_destroy",
               "gpd_last_error_string", "gpd_ctx_reload_tables", "gpd_default_tables",
+              "gpd_ctx_set_options", "gpd_ctx_add_decoders",
               "gpd_pcap_header", "gpd_pcap_index", "gpd_decode_pcap", "gpd_host_register", "gpd_host_bind_local",
               "gpd_flow_create", "gpd_flow_insert", "gpd_flow_export", "gpd_flow_stats_get",
               "gpd_ip4_fragments"):
@@ -38,7 +39,7 @@ def test_library_exports_every_declared_symbol():
     lib = C.CDLL(_lib.LIB_PATH)
     missing = [f for f in declared_functions() if not hasattr(lib, f)]
     assert not missing, missing
-    assert lib.gpd_abi_version() == 7
+    assert lib.gpd_abi_version() == 8
 
 
 def test_python_binding_covers_the_header():
@@ -95,7 +96,10 @@ def test_c_host_program_on_the_abi(tmp_path):
     """tests/c/abi_host: a plain C program (no Python, no torch in its process — the cgo case)
     decodes through gpd_decode on its own hipMalloc'ed buffers and stream and through
     gpd_decode_host and gpd_decode_pcap (the same packets as a capture file); all must equal the
-    oracle bit for bit, and the device results must build a consistent flow table."""
+    oracle bit for bit, and the device results must build a consistent flow table.  Then (ABI 8)
+    a second context registers UDP 8472 as VXLAN, reloads its tables, adds the VXLAN decoder in
+    place and flips IgnoreUnsupported both ways, each step host and device against the oracle on
+    the same mutated tables; and it decodes an all-empty batch."""
     import golden_cases as G
     from gopacket_amd import synth
     from gopacket_amd.batch import PacketBatch
@@ -113,6 +117,12 @@ def test_c_host_program_on_the_abi(tmp_path):
     from gopacket_amd.layers import ip_protocol_name
     pkts += [bytes.fromhex(c["hex"]) for c in EC.load()]
     pkts += ES.packets()
+    # VXLAN on UDP port 8472 (not a default port): the reconfiguration step registers it
+    vx = synth.make_vxlan(96)
+    for i in range(vx.n):
+        p = bytearray(vx.packet(i))
+        p[36:38] = (8472).to_bytes(2, "big")
+        pkts.append(bytes(p))
     names = tmp_path / "ipproto_names.txt"
     names.write_text("".join(ip_protocol_name(p) + "\n" for p in range(256)))
     for decoders, options in ((0xFFF, 0), (0x3FF, 1), (0x1 | 0x4 | 0x400 | 0x20 | 0x40 | 0x100, 0)):
@@ -125,12 +135,15 @@ def test_c_host_program_on_the_abi(tmp_path):
             fh.write(b.offset.astype(np.uint32).tobytes())
             fh.write(b.caplen.astype(np.uint32).tobytes())
         errs = tmp_path / f"errors_{decoders:x}_{options}.txt"
-        r = subprocess.run([exe, str(f), str(errs), str(names)], capture_output=True, text=True, timeout=90)
+        r = subprocess.run([exe, str(f), str(errs), str(names), "8472"], capture_output=True, text=True,
+                           timeout=90)
         assert r.returncode == 0, r.stdout + r.stderr
         words = r.stdout.split()
         assert words[:3] == ["abi_host", "ok", str(b.n)], r.stdout
         assert int(words[3]) > 100, r.stdout  # the mixed traffic holds many TCP/UDP flows
         assert int(words[4]) > 100, r.stdout  # ip4defrag's fragments and the fuzz frames
+        if decoders & 0x80:  # the in-place reconfiguration reached VXLAN on the registered port
+            assert int(words[5]) >= 96, r.stdout
         # the C host's error texts (from status + gpd_detail) == the oracle's, packet by packet
         ref = O.decode(b, 17, decoders, options, ext=True, nthreads=8)
         want = {i: str(ref.err(i)) for i in range(b.n) if (int(ref.status[i]) & 3) == 2}

@@ -188,6 +188,53 @@ def test_decode_tpv3_matches_oracle(add_vlan):
         assert tagged and all(res.decoded(j)[:2] == [L.LayerTypeEthernet, L.LayerTypeDot1Q] for j in tagged[:50])
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("device_walk,register", [(1, False), (0, False), (1, True)])
+def test_decode_tpv3_detail_matches_oracle(device_walk, register):
+    """gpd_detail through gpd_decode_tpv3 (afpacket.go:300-333's ZeroCopyReadPacketData loop
+    feeding DecodeLayers): one packet per reference error site and > 12-layer stacks among mixed
+    traffic in a ring; the detail records and the error texts rebuilt from status + detail equal
+    the oracle's — device and host block walks, staged and registered (direct) result arrays."""
+    import error_sites as ES
+    from gopacket_amd import _lib, afpacket as A
+    from gopacket_amd import parser as P
+    from test_parity_gpu import assert_detail, detail_rows
+    pk = _packets(1500, seed=11)
+    for k, p in enumerate(ES.packets()):
+        pk.insert(23 * k + 7, p)
+    arr, used = synth.make_tpv3_ring(pk, 1 << 16, 64)
+    ring = A.TPv3Ring(arr, 1 << 16, 64)
+    parser = P.NewDecodingLayerParser(L.LayerTypeEthernet, *[P.DECODER_BY_NAME[k]() for k in P.DECODER_BY_NAME])
+    parser.Tuning = {"device_walk": device_walk}
+    out = ci = None
+    arrays = []
+    if register:  # every result and capture-info array registered: the D2H lands in them directly
+        from gopacket_amd.results import DETAIL_DTYPE, BatchResult
+        m = 1 << 16
+        out = BatchResult(np.zeros(m, np.uint32), np.zeros(m, np.uint64), np.zeros(m, np.uint64),
+                          np.zeros(m, np.uint64), np.zeros(m, np.uint32), None, np.zeros(m, np.uint32),
+                          np.zeros(m, DETAIL_DTYPE))
+        ci = A.CaptureInfo.alloc(m)
+        arrays = [out.status, out.layers, out.net_hash, out.tp_hash, out.csum, out.hdr_off, out.detail,
+                  ci.offset, ci.caplen, ci.length, ci.ts_ns, ci.ifindex, ci.vlan, ci.vlan_tci]
+        for a in arrays:
+            _lib.check(_lib.lib.gpd_host_register(parser.ctx().h, a.ctypes.data, a.nbytes), "register")
+    try:
+        res, ci, nblk = parser.DecodeTPv3(ring, max_n=1 << 16, out=out, ci=ci, detail=True)
+    finally:
+        for a in arrays:
+            _lib.lib.gpd_host_unregister(parser.ctx().h, a.ctypes.data)
+    ref_pk, rblk = T.read_loop(arr.tobytes(), 1 << 16, 64, 0, None, False)
+    assert nblk == rblk and len(res) == len(ref_pk) == len(pk)
+    ref = O.decode(PacketBatch.from_packets([r["data"] for r in ref_pk]), L.LayerTypeEthernet,
+                   parser.decoders, 0, ext=True, nthreads=8)
+    for f in ("status", "layers", "net_hash", "tp_hash", "csum", "hdr_off"):
+        assert (getattr(res, f) == getattr(ref, f)).all(), f
+    rows = detail_rows(ref.status)
+    assert len(rows) >= len(ES.packets())
+    assert_detail(res, ref)
+
+
 def _decode_both(arr, bs, nb, first, register=False, **kw):
     """DecodeTPv3 with the walk on the device and on the host: equal results, capture info,
     block counts and errors.  Returns (path of the device-walk call, packets, blocks)."""

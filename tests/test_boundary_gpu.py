@@ -148,3 +148,23 @@ def test_host_bind_local_places_pages_on_the_gpu_node():
     assert pages.get(node.value, 0) >= 0.9 * sum(pages.values()), (node.value, pages)
     del a
     mm.close()
+
+
+def test_round_kernel_tile_longer_than_its_round_field():
+    """ro_kernel keeps a header's round of the tile's byte run in 16 bits.  A
+    64-packet tile of 9-MiB frames back to back spans 576 MiB = 73,728 rounds of 8 KiB, so the
+    later lanes' header rounds pass 0xFFFF: such a tile goes to the fallback list whole.  IMIX
+    frames (their IPv4 Length bounds the decode) sit at the start of each 9-MiB slot; both the
+    forced round kernel and the automatic choice equal the oracle."""
+    imix = synth.make_imix(64, seed=0x5EED0641)
+    slot = 9 << 20
+    n = imix.n
+    data = np.zeros(n * slot + 64, np.uint8)
+    off = np.arange(n, dtype=np.uint64) * slot
+    for i in range(n):
+        p = np.frombuffer(imix.packet(i), np.uint8)
+        data[off[i]:off[i] + len(p)] = p
+    b = PacketBatch.from_arrays(data, off.astype(np.uint32), np.full(n, slot, np.uint32), n * slot)
+    assert (b.data_len >> 13) > 0xFFFF
+    for tuning in (dict(header_once=2), None):
+        run_both(b, L.LayerTypeEthernet, ALL, 0, ext=False, tuning=tuning)

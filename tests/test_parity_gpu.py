@@ -519,6 +519,54 @@ def test_mutated_dispatch_tables():
     run_both(PacketBatch.from_packets(pk), tables=t)
 
 
+def test_reconfigure_in_place_keeps_tables_and_context():
+    """ABI 8 through the Python parser (parser.go:182-202, layers/ports.go:126-128): register a
+    UDP port as VXLAN and reload the tables, add the VXLAN decoder, then flip IgnoreUnsupported
+    both ways.  The context is the same gpd_ctx throughout (no re-creation that would drop the
+    reloaded tables), and every step equals the oracle on the mutated tables, on the fast path
+    (ext=False) and the generic one."""
+    from gopacket_amd import parser as P
+    saved = L.TABLES.copy()
+    try:
+        pk = _golden_packets()
+        vx = synth.make_vxlan(128)
+        for i in range(vx.n):
+            q = bytearray(vx.packet(i))
+            q[36:38] = (8472).to_bytes(2, "big")
+            pk.append(bytes(q))
+        b = PacketBatch.from_packets(pk)
+        p = P.NewDecodingLayerParser(L.LayerTypeEthernet, P.Ethernet(), P.Dot1Q(), P.IPv4(), P.IPv6(),
+                                     P.TCP(), P.UDP(), P.Payload())
+        p.DecodeBatch(b)  # the context exists before anything changes
+        h = p.ctx().h.value
+        L.RegisterUDPPortLayerType(8472, L.LayerTypeVXLAN)
+        p.reload_tables()
+        p.AddDecodingLayer(P.VXLAN())
+        for ign in (True, False, True):
+            p.IgnoreUnsupported = ign
+            ref = O.decode(b, L.LayerTypeEthernet, p.decoders, p.options, tables=L.TABLES, ext=True,
+                           nthreads=8)
+            assert any(L.LayerTypeVXLAN in ref.decoded(i) for i in range(len(pk) - 8, len(pk)))
+            for e in (False, True):
+                dev = p.DecodeBatch(b, ext=e)
+                assert_same(dev, ref, b, e)
+            assert_same(p.DecodeBatchHost(b, detail=True), ref, b, ext=False)
+            assert p.ctx().h.value == h, "the context was re-created"
+    finally:
+        L.TABLES.udp_port[:] = saved.udp_port
+
+
+def test_all_empty_batch():
+    """A batch whose every packet is empty (CapLen 0, data_len 0): Ethernet's "too small" error
+    for each, on the device and host paths."""
+    b = PacketBatch.from_packets([b""] * 37)
+    assert b.data_len == 0
+    ref = run_both(b)
+    assert all(str(ref.err(i)) == "Ethernet packet too small" for i in range(b.n))
+    host = _parser().DecodeBatchHost(b, detail=True)
+    assert_same(host, O.decode(b, L.LayerTypeEthernet, ALL, 0, ext=True), b, ext=False)
+
+
 def test_options_no_checksums_no_hashes():
     b = synth.make_mixed(3000)
     for opt in (256, 512, 768, 769):
