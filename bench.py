@@ -268,29 +268,47 @@ def bench_record36(parser, dev_batch, n, local, stream, out, args, records=False
             "read_frac": round(rb / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
-def attainable(n: int, read_bytes: int, local: int, achieved_gbps: float):
+def attainable(n: int, read_bytes: int, local: int, achieved_gbps: float, soa: bool = False):
     """The streaming ceiling for this launch's traffic shape on this box (libgpd_probe.so): the
-    same read bytes per 64-packet tile as one contiguous run and the same 2 KiB of records per
-    tile, no decode, no packet boundaries, after its own clock settle.  `frac` of the decode is
-    read against peak; `of_attainable` against this.  None without the probe."""
+    same read bytes per 64-packet tile as one contiguous run and the same 32 B of results per
+    packet in the same form as the launch (two 16-B record stores per lane, or the five SoA
+    arrays), no decode, no packet boundaries, after its own clock settle.  `frac` of the decode is
+    read against peak; `of_attainable` against this.  An SoA line carries the
+    record-form probe beside it (`record_form_probe`).  None without the probe."""
     import ctypes as C
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gopacket_amd", "libgpd_probe.so")
     if not os.path.exists(path):
         return None
     lib = C.CDLL(path)
-    lib.gpd_probe_stream.argtypes = [C.c_int, C.c_uint32, C.c_uint32, C.c_int, C.c_float, C.POINTER(C.c_float)]
+    lib.gpd_probe_stream2.argtypes = [C.c_int, C.c_uint32, C.c_uint32, C.c_int, C.c_float, C.c_int,
+                                      C.POINTER(C.c_float)]
     ntiles = (n + 63) // 64
     per_tile = -(-read_bytes // ntiles)
-    ms = C.c_float(0.0)
-    rc = lib.gpd_probe_stream(local, ntiles, per_tile, 20, 150.0, C.byref(ms))
-    if rc != 0 or ms.value <= 0:
-        return {"error": f"gpd_probe_stream rc={rc}"}
-    gbps = (ntiles * per_tile + ntiles * 2048) / (ms.value * 1e-3) / 1e9
-    return {"GBps": round(gbps, 1), "frac_of_peak": round(gbps / HBM_PEAK_GBS, 4),
-            "of_attainable": round(achieved_gbps / gbps, 4), "probe_ms": round(ms.value, 4),
-            "read_bytes_per_tile": per_tile, "write_bytes_per_tile": 2048,
-            "probe": "gpd_probe_stream: contiguous 16-B-per-lane nt loads of each tile's read bytes + "
-                     "two 16-B nt record stores per lane, no decode (2 and 4 workgroups per CU, best)"}
+
+    def probe(form_soa):
+        ms = C.c_float(0.0)
+        rc = lib.gpd_probe_stream2(local, ntiles, per_tile, 20, 150.0, int(form_soa), C.byref(ms))
+        if rc != 0 or ms.value <= 0:
+            return None, rc
+        return (ntiles * per_tile + ntiles * 2048) / (ms.value * 1e-3) / 1e9, ms.value
+
+    gbps, ms = probe(soa)
+    if gbps is None:
+        return {"error": f"gpd_probe_stream2 rc={ms}"}
+    out = {"GBps": round(gbps, 1), "frac_of_peak": round(gbps / HBM_PEAK_GBS, 4),
+           "of_attainable": round(achieved_gbps / gbps, 4), "probe_ms": round(ms, 4),
+           "read_bytes_per_tile": per_tile, "write_bytes_per_tile": 2048,
+           "result_form": "SoA arrays" if soa else "gpd_record",
+           "probe": "gpd_probe_stream2: contiguous 16-B-per-lane nt loads of each tile's read bytes + "
+                    + ("the five SoA result arrays (u32, u64, u64, u64, u32) as nt stores"
+                       if soa else "two 16-B nt record stores per lane")
+                    + ", no decode (2 and 4 workgroups per CU, best)"}
+    if soa:  # the record-form probe too, for comparison with earlier rounds' lines
+        g2, ms2 = probe(False)
+        if g2 is not None:
+            out["record_form_probe"] = {"GBps": round(g2, 1), "probe_ms": round(ms2, 4),
+                                        "of_attainable": round(achieved_gbps / g2, 4)}
+    return out
 
 
 SIDE_CONFIGS = ("tcp64", "imix", "vxlan", "pcap64")  # timed beside the default line (N = 1)
@@ -340,7 +358,7 @@ def bench_side(config, parser, args, local, stream):
            "decode_errors_in_batch": int(np.count_nonzero((st & 3) != 0)),
            "settle_ms": settled, "generate_s": round(t_gen, 2)}
     if not args.no_probe:
-        out["attainable"] = attainable(n, read, local, out["achieved_GBps"])
+        out["attainable"] = attainable(n, read, local, out["achieved_GBps"], soa=not aos)
     tr = load_traffic(config)
     if tr and tr["read"] and tr["write"]:
         out["traffic"] = int(tr["read"]) + int(tr["write"])
@@ -1319,7 +1337,7 @@ def main():
             out["pcie_inclusive"] = bench_host(parser, batch, n, "registered", 3, 1)
     if not args.ablate and not args.lean and not args.no_probe:
         rf = out["roofline"]
-        rf["attainable"] = attainable(n, rf["algorithmic_read_bytes"], local, rf["achieved"])
+        rf["attainable"] = attainable(n, rf["algorithmic_read_bytes"], local, rf["achieved"], soa=not aos)
     if pcap_info:
         out["pcap"] = pcap_info
         if args.replay:

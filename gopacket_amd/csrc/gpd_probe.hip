@@ -53,6 +53,39 @@ __global__ __launch_bounds__(256) void probe_k(const v4u *__restrict__ in, v4u *
   }
 }
 
+// The same with the results as the five SoA arrays of gpd_result (status u32, layers u64,
+// net_hash u64, tp_hash u64, csum u32: the same 32 B per packet as five coalesced stores per
+// tile), the form BASELINE config 3 asks for.
+template <int MAXC>
+__global__ __launch_bounds__(256) void probe_soa_k(const v4u *__restrict__ in, uint8_t *__restrict__ rec,
+                                                   uint32_t ntiles, uint32_t ctile) {
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint32_t nw = gridDim.x * 4u;
+  const uint64_t n = (uint64_t)ntiles * 64u;
+  uint32_t *st = reinterpret_cast<uint32_t *>(rec), *cs = st + n;
+  uint64_t *ly = reinterpret_cast<uint64_t *>(cs + n), *nh = ly + n, *th = nh + n;
+  for (uint32_t t = blockIdx.x * 4u + wave; t < ntiles; t += nw) {
+    const v4u *p = in + (uint64_t)t * ctile;
+    uint32_t x = 0;
+    for (uint32_t c0 = 0; c0 < ctile; c0 += 64u * MAXC) {
+      v4u v[MAXC];
+#pragma unroll
+      for (int j = 0; j < MAXC; j++) {
+        const uint32_t c = c0 + 64u * j + lane;
+        v[j] = c < ctile ? __builtin_nontemporal_load(p + c) : v4u{0u, 0u, 0u, 0u};
+      }
+#pragma unroll
+      for (int j = 0; j < MAXC; j++) x ^= v[j].x + v[j].y + v[j].z + v[j].w;
+    }
+    const uint64_t i = (uint64_t)t * 64u + lane;
+    __builtin_nontemporal_store(x, st + i);
+    __builtin_nontemporal_store((uint64_t)x * 3u, ly + i);
+    __builtin_nontemporal_store((uint64_t)x * 5u, nh + i);
+    __builtin_nontemporal_store((uint64_t)x * 7u, th + i);
+    __builtin_nontemporal_store(x ^ 9u, cs + i);
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -61,8 +94,18 @@ extern "C" {
 // records each, at 2 and 4 workgroups per CU, `reps` timed launches after `warm_ms` of untimed
 // ones; *best_ms is the fastest configuration's mean launch time.  0 on success, else the HIP
 // error code.  Allocates and frees its own buffers.
+int gpd_probe_stream2(int device, uint32_t ntiles, uint32_t read_bytes_per_tile, int reps, float warm_ms,
+                      int soa, float *best_ms);
+
 int gpd_probe_stream(int device, uint32_t ntiles, uint32_t read_bytes_per_tile, int reps, float warm_ms,
                      float *best_ms) {
+  return gpd_probe_stream2(device, ntiles, read_bytes_per_tile, reps, warm_ms, 0, best_ms);
+}
+
+// gpd_probe_stream with the results stored as two 16-B records per lane (soa = 0, the gpd_record
+// form) or as the five SoA arrays (soa = 1).
+int gpd_probe_stream2(int device, uint32_t ntiles, uint32_t read_bytes_per_tile, int reps, float warm_ms,
+                      int soa, float *best_ms) {
   hipError_t e = hipSetDevice(device);
   if (e != hipSuccess) return (int)e;
   const uint32_t ctile = (read_bytes_per_tile + 15u) / 16u;
@@ -80,8 +123,15 @@ int gpd_probe_stream(int device, uint32_t ntiles, uint32_t read_bytes_per_tile, 
     const uint32_t g = (uint32_t)prop.multiProcessorCount * (uint32_t)wpc;
     const uint32_t pl = (ctile + 63u) / 64u;  // chunks per lane per tile
     auto launch = [&] {  // a 64-B-frame tile (4.5 KiB) in one round; longer tiles in rounds of 8 KiB
-      if (pl <= 5u) hipLaunchKernelGGL(probe_k<5>, dim3(g), dim3(256), 0, 0, in, rec, ntiles, ctile);
-      else hipLaunchKernelGGL(probe_k<8>, dim3(g), dim3(256), 0, 0, in, rec, ntiles, ctile);
+      if (soa) {
+        uint8_t *r8 = reinterpret_cast<uint8_t *>(rec);
+        if (pl <= 5u) hipLaunchKernelGGL(probe_soa_k<5>, dim3(g), dim3(256), 0, 0, in, r8, ntiles, ctile);
+        else hipLaunchKernelGGL(probe_soa_k<8>, dim3(g), dim3(256), 0, 0, in, r8, ntiles, ctile);
+      } else if (pl <= 5u) {
+        hipLaunchKernelGGL(probe_k<5>, dim3(g), dim3(256), 0, 0, in, rec, ntiles, ctile);
+      } else {
+        hipLaunchKernelGGL(probe_k<8>, dim3(g), dim3(256), 0, 0, in, rec, ntiles, ctile);
+      }
     };
     // untimed launches for warm_ms (the clocks settle, as bench.py does for the decode)
     float spent = 0.0f;

@@ -172,7 +172,7 @@ def test_probe_library_exports_its_entry_points():
     import ctypes as C
     from gopacket_amd import build
     lib = C.CDLL(build.build_probe())
-    for sym in ("gpd_probe_stream", "gpd_probe_stream_ex"):
+    for sym in ("gpd_probe_stream", "gpd_probe_stream2", "gpd_probe_stream_ex"):
         assert hasattr(lib, sym), sym
 
 

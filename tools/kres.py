@@ -6,7 +6,7 @@ import sys
 
 ROOT = __file__.rsplit("/tools/", 1)[0]
 r = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-I", ROOT + "/include",
-                    "-c", ROOT + "/gopacket_amd/csrc/gpd_kernels.hip", "-o", "/tmp/kres.o",
+                    "-c", ROOT + "/gopacket_amd/csrc/gpd_kernels.hip", "-o", "/tmp/kres.o"] + __import__("os").environ.get("GPD_EXTRA_CFLAGS", "").split() + [
                     "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True)
 cur, rows = None, []
 for line in r.stderr.splitlines():

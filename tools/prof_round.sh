@@ -20,7 +20,10 @@ run() {  # name, rocprofv3 args...
 run kt --kernel-trace --stats &&
 run fetch --pmc FETCH_SIZE &&
 run write --pmc WRITE_SIZE &&
-run sq --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY
+run sq --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY &&
+# clock and occupancy: effective shader clock = GRBM_GUI_ACTIVE / 8 XCDs / kernel time
+# (MI355X_MICROARCH.md "DVFS give-back"); SQ_WAVE_CYCLES (quad-cycles) over it: resident waves per CU
+run clk --pmc GRBM_GUI_ACTIVE GRBM_COUNT SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAVES
 # optional LDS pass (PROF_LDS=1): bank conflicts and LDS-array cycles of the decode kernel
 if [ "${PROF_LDS:-0}" = 1 ]; then
   run lds --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES

@@ -63,6 +63,15 @@ def summarize(d):
     lds, _ = counters(d, "lds")
     if lds:
         s["lds_per_launch"] = lds
+    clk, _ = counters(d, "clk")
+    if clk:
+        s["clk_per_launch"] = clk
+        dec = [v for k, v in s["kernels"].items() if any(x in k for x in ("rs_kernel", "ro_kernel", "decode_kernel"))]
+        if dec and "GRBM_GUI_ACTIVE" in clk:  # the decode kernel's mean time from the kt pass
+            us = max(dec, key=lambda v: v["calls"])["avg_us"]
+            s["effective_clock_ghz"] = clk["GRBM_GUI_ACTIVE"] / 8 / (us * 1e3)
+            if "SQ_WAVE_CYCLES" in clk:  # quad-cycles of residency, summed over waves
+                s["mean_resident_waves_per_cu"] = 4 * clk["SQ_WAVE_CYCLES"] / (clk["GRBM_GUI_ACTIVE"] / 8 * 256)
     return s
 
 
