@@ -132,6 +132,52 @@ func (p *BatchDecodingLayerParser) AddDecodingLayer(d gopacket.DecodingLayer) er
 	return nil
 }
 
+// kindTypes: each engine decoder kind and the CanDecode set it registers (gpd.h GPD_DEC_*).
+var kindTypes = map[uint32][]gopacket.LayerType{
+	DecEthernet: {layers.LayerTypeEthernet},
+	DecDot1Q:    {layers.LayerTypeDot1Q},
+	DecIPv4:     {layers.LayerTypeIPv4},
+	DecIPv6:     {layers.LayerTypeIPv6},
+	DecIPv6Ext: {layers.LayerTypeIPv6HopByHop, layers.LayerTypeIPv6Routing,
+		layers.LayerTypeIPv6Fragment, layers.LayerTypeIPv6Destination},
+	DecTCP:      {layers.LayerTypeTCP},
+	DecUDP:      {layers.LayerTypeUDP},
+	DecVXLAN:    {layers.LayerTypeVXLAN},
+	DecPayload:  {gopacket.LayerTypePayload},
+	DecFragment: {gopacket.LayerTypeFragment},
+	DecICMPv4:   {layers.LayerTypeICMPv4},
+	DecLLC:      {layers.LayerTypeLLC},
+}
+
+// SetDecodingLayerContainer mirrors (*DecodingLayerParser).SetDecodingLayerContainer
+// (parser.go:236-242): the decoders dlc holds replace the registered set, in place
+// (gpd_ctx_set_decoders; device and reloaded tables kept).  The engine registers decoder kinds
+// whole: a container holding a kind for only part of its CanDecode set (IPv6ExtensionSkipper for
+// some of 46..49) has no engine equivalent and is refused.
+func (p *BatchDecodingLayerParser) SetDecodingLayerContainer(dlc gopacket.DecodingLayerContainer) error {
+	var mask uint32
+	for bit, types := range kindTypes {
+		held := 0
+		for _, t := range types {
+			if d, ok := dlc.Decoder(t); ok {
+				if b, err := decoderBit(d); err == nil && b == bit {
+					held++
+				}
+			}
+		}
+		if held == len(types) {
+			mask |= bit
+		} else if held > 0 {
+			return fmt.Errorf("gpdecode: the container holds decoder kind %#x for only %d of its %d layer types", bit, held, len(types))
+		}
+	}
+	if rc := C.gpd_ctx_set_decoders(p.ctx, C.uint32_t(mask)); rc != C.GPD_OK {
+		return lastError("gpd_ctx_set_decoders", rc)
+	}
+	p.decoders = mask
+	return nil
+}
+
 // Device is the GPU the parser decodes on.
 func (p *BatchDecodingLayerParser) Device() int { return p.device }
 

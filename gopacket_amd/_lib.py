@@ -53,6 +53,7 @@ EXPORTS = {
     "gpd_ctx_reload_tables": (C.c_int, [C.c_void_p, C.POINTER(GpdConfig)]),
     "gpd_ctx_set_options": (C.c_int, [C.c_void_p, C.c_uint32]),
     "gpd_ctx_add_decoders": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "gpd_ctx_set_decoders": (C.c_int, [C.c_void_p, C.c_uint32]),
     "gpd_ctx_destroy": (C.c_int, [C.c_void_p]),
     "gpd_decode": (C.c_int, [C.c_void_p, C.POINTER(GpdBatch), C.POINTER(GpdResult), C.c_void_p]),
     "gpd_decode_host": (C.c_int, [C.c_void_p, C.POINTER(GpdBatch), C.POINTER(GpdResult)]),

@@ -402,6 +402,15 @@ int gpd_ctx_set_options(gpd_ctx *ctx, uint32_t options) {
   return GPD_OK;
 }
 
+int gpd_ctx_set_decoders(gpd_ctx *ctx, uint32_t decoders) {
+  if (!ctx) return set_err(GPD_ERR_INVALID, "gpd_ctx_set_decoders: ctx is NULL");
+  if (decoders & ~GPD_DEC_ALL)
+    return set_err(GPD_ERR_INVALID, "gpd_ctx_set_decoders: unknown decoder bits 0x%x", decoders);
+  if (decoders == ctx->decoders) return GPD_OK;
+  ctx->decoders = decoders;
+  return build_image(ctx);
+}
+
 int gpd_ctx_add_decoders(gpd_ctx *ctx, uint32_t decoders) {
   if (!ctx) return set_err(GPD_ERR_INVALID, "gpd_ctx_add_decoders: ctx is NULL");
   if (decoders & ~GPD_DEC_ALL)

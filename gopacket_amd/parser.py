@@ -24,6 +24,7 @@ import numpy as np
 from . import layers as L
 from ._lib import GPD_ERR_PCAP, GpdBatch, GpdConfig, GpdResult, check, lib
 from .batch import PAD, PacketBatch
+from .errors import UnsupportedLayerType
 from .results import DETAIL_DTYPE, EXT_DTYPE, RECORD_DTYPE, BatchResult
 
 DEC_ETHERNET, DEC_DOT1Q, DEC_IPV4, DEC_IPV6, DEC_IPV6_EXT = 1, 2, 4, 8, 16
@@ -94,6 +95,120 @@ DECODER_BY_NAME = {c.__name__: c for c in (Ethernet, Dot1Q, IPv4, IPv6, IPv6Exte
                                             UDP, VXLAN, Payload, Fragment, ICMPv4, LLC)}
 
 
+# ---- DecodingLayerContainer (parser.go:54-177) ------------------------------------------------
+class DecodingLayerContainer:
+    """parser.go:56-67: Put / Decoder / LayersDecoder.  Put returns the container (the reference's
+    value-receiver convention).  The engine registers decoder *kinds*: `engine_mask()` is the set
+    of kinds the container holds for every type of their CanDecode set."""
+
+    def Put(self, d) -> "DecodingLayerContainer":
+        raise NotImplementedError
+
+    def Decoder(self, typ: int):
+        raise NotImplementedError
+
+    def LayersDecoder(self, first: int, df=None, device: int = 0) -> "DecodingLayerFunc":
+        """layers_decoder.go:11-101: a DecodingLayerFunc over this container's decoders."""
+        return DecodingLayerFunc(self, first, df, device)
+
+    def engine_mask(self) -> int:
+        m = 0
+        for cls in DECODER_BY_NAME.values():
+            held = [isinstance(self.Decoder(t)[0], cls) for t in cls.can_decode]
+            if all(held):
+                m |= cls.bit
+            elif any(held):  # (e.g. IPv6ExtensionSkipper for some of 46..49 only)
+                raise ValueError(f"{cls.__name__} is held for only part of its CanDecode set "
+                                 f"{cls.can_decode}: the engine registers decoder kinds whole")
+        return m
+
+
+class DecodingLayerSparse(DecodingLayerContainer):
+    """parser.go:69-108: a slice indexed by LayerType."""
+
+    def __init__(self, layers=None):
+        self.dl = list(layers or [])
+
+    def Put(self, d):
+        for t in d.CanDecode():
+            if t >= len(self.dl):
+                self.dl.extend([None] * (t + 1 - len(self.dl)))
+            self.dl[t] = d
+        return self
+
+    def Decoder(self, typ):
+        if 0 <= typ < len(self.dl) and self.dl[typ] is not None:
+            return self.dl[typ], True
+        return None, False
+
+
+class DecodingLayerArray(DecodingLayerContainer):
+    """parser.go:110-146: (type, decoder) pairs searched linearly; a Put of a type already held
+    replaces its decoder in place."""
+
+    def __init__(self):
+        self.dl = []
+
+    def Put(self, d):
+        for t in d.CanDecode():
+            for e in self.dl:
+                if e[0] == t:
+                    e[1] = d
+                    break
+            else:
+                self.dl.append([t, d])
+        return self
+
+    def Decoder(self, typ):
+        for t, d in self.dl:
+            if t == typ:
+                return d, True
+        return None, False
+
+
+class DecodingLayerMap(DecodingLayerContainer):
+    """parser.go:148-169: a map by LayerType (NewDecodingLayerParser's default)."""
+
+    def __init__(self):
+        self.dl = {}
+
+    def Put(self, d):
+        for t in d.CanDecode():
+            self.dl[t] = d
+        return self
+
+    def Decoder(self, typ):
+        d = self.dl.get(typ)
+        return d, d is not None
+
+
+class DecodingLayerFunc:
+    """parser.go:52 / layers_decoder.go:11-101: fn(data, decoded) -> (LayerType, error) for one
+    packet, decoded on the GPU with the container's decoders: (first, None) leaving `decoded`
+    untouched when no decoder takes `first`; (0, err) on a decode error; (typ, None) when no
+    decoder takes typ; (0, None) on success.  A Truncated packet calls df.SetTruncated()."""
+
+    def __init__(self, dlc: DecodingLayerContainer, first: int, df, device: int):
+        self.first, self.df = int(first), df
+        self.has_first = dlc.Decoder(self.first)[1]
+        self.p = DecodingLayerParser(self.first, device=device)
+        self.p._mask = dlc.engine_mask()
+
+    def __call__(self, data: bytes, decoded: list):
+        if not self.has_first:
+            return self.first, None
+        res = self.p.DecodeBatch(PacketBatch.from_packets([data]), detail=True)
+        decoded[:] = res.decoded(0)
+        if res.truncated(0) and self.df is not None:
+            self.df.SetTruncated()
+        st = int(res.status[0]) & 3
+        if st == 2:
+            return L.LayerTypeZero, res.err(0)
+        if st == 1:
+            return res.stop_type(0), None
+        return L.LayerTypeZero, None
+
+
 def decoder_mask(decoders) -> int:
     m = 0
     for d in decoders:
@@ -145,6 +260,15 @@ class _Ctx:
         if mask | self.mask != self.mask:
             check(lib.gpd_ctx_add_decoders(self.h, mask), "gpd_ctx_add_decoders")
             self.mask |= mask
+
+    def set_decoders(self, mask: int):
+        if mask == self.mask:
+            return
+        if mask & ~self.mask == mask ^ self.mask:  # only added: AddDecodingLayer
+            self.add_decoders(mask)
+            return
+        check(lib.gpd_ctx_set_decoders(self.h, mask), "gpd_ctx_set_decoders")
+        self.mask = mask
 
     def __del__(self):
         h = getattr(self, "h", None)
@@ -248,11 +372,28 @@ class DecodingLayerParser:
         self.device = device
         self._ctx: Optional[_Ctx] = None
         self._tables = L.TABLES.copy()
+        self._dlc: DecodingLayerContainer = DecodingLayerMap()  # parser.go:226 (the default)
+        for d in decoders:
+            d = DECODER_BY_NAME[d]() if isinstance(d, str) else (d() if isinstance(d, type) else d)
+            self._dlc = self._dlc.Put(d)
 
     # --- registration (parser.go:197-241) ---------------------------------------
     def AddDecodingLayer(self, d) -> None:
-        """parser.go:197-202; applied to an existing context in place (gpd_ctx_add_decoders)."""
+        """parser.go:197-202 (the container's Put); applied to an existing context in place
+        (gpd_ctx_add_decoders)."""
+        d = DECODER_BY_NAME[d]() if isinstance(d, str) else (d() if isinstance(d, type) else d)
         self._mask |= decoder_mask([d])
+        self._dlc = self._dlc.Put(d)
+
+    def SetDecodingLayerContainer(self, dlc: DecodingLayerContainer) -> None:
+        """parser.go:236-242: the container's decoders replace the registered set
+        (gpd_ctx_set_decoders on an existing context: device and tables kept)."""
+        self._dlc = dlc
+        self._mask = dlc.engine_mask()
+
+    def SetTruncated(self) -> None:
+        """parser.go:204-209 (DecodeFeedback)."""
+        self.Truncated = True
 
     @property
     def decoders(self) -> int:
@@ -278,11 +419,11 @@ class DecodingLayerParser:
         decoders apply in place (gpd_ctx_set_options / gpd_ctx_add_decoders), so the table
         snapshot, tuning and staging survive them as the reference parser's state does."""
         c = self._ctx
-        if c is None or (c.device, c.first) != (self.device, self.first) or c.mask & ~self._mask:
+        if c is None or (c.device, c.first) != (self.device, self.first):
             self._ctx = c = _Ctx(self.device, self.first, self._mask, self.options, self._tables)
             c.tuned = None
         else:
-            c.add_decoders(self._mask)
+            c.set_decoders(self._mask)
             c.set_options(self.options)
         if self._ctx.tuned != self.Tuning:
             self._apply_tuning()
@@ -426,6 +567,11 @@ class DecodingLayerParser:
     def DecodeLayers(self, data: bytes, decoded: list):
         """parser.go:302-316 for one packet: fills `decoded`, sets self.Truncated, returns the
         error value (None on success)."""
+        self.Truncated = False
+        if not any(c.bit & self._mask and self.first in c.can_decode for c in DECODER_BY_NAME.values()):
+            # layers_decoder.go:12-16: no decoder for `first` returns before `decoded` is
+            # truncated, so the caller's slice keeps its previous contents
+            return None if self.IgnoreUnsupported else UnsupportedLayerType(self.first)
         res = self.DecodeBatch(PacketBatch.from_packets([data]), detail=True)
         decoded[:] = res.decoded(0)
         self.Truncated = res.truncated(0)

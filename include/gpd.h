@@ -19,6 +19,7 @@
  *   gpd_ctx_set_options   assigning parser.IgnoreUnsupported / IgnorePanic  parser.go:182-195,
  *                           336-350 (plain fields: the parser, its decoders and the tables stay)
  *   gpd_ctx_add_decoders  (*DecodingLayerParser).AddDecodingLayer       parser.go:197-202
+ *   gpd_ctx_set_decoders  (*DecodingLayerParser).SetDecodingLayerContainer parser.go:236-242
  *   gpd_decode            (*DecodingLayerParser).DecodeLayers        parser.go:302-316
  *                         (loop: layers_decoder.go:60-79), fused with
  *                         TCP.ComputeChecksum                          layers/tcp.go:193-195,
@@ -54,8 +55,8 @@ extern "C" {
                               gpd_tuning.device_walk, gpd_result.records; 6: outputs follow the
                               objects as a failing call leaves them; ext err_obj/err_wrote/err_off;
                               7: gpd_result.detail (error arguments and deep stacks without ext);
-                              8: gpd_ctx_set_options, gpd_ctx_add_decoders (in place: device,
-                              tables and staging kept) */
+                              8: gpd_ctx_set_options, gpd_ctx_add_decoders, gpd_ctx_set_decoders
+                              (in place: device, tables and staging kept) */
 
 /* ---- gopacket LayerType numbers (layertypes.go:14-154, decode.go:105-116) ---- */
 #define GPD_LT_ZERO            0
@@ -371,6 +372,10 @@ int  gpd_ctx_set_options(gpd_ctx *ctx, uint32_t options);
  * The dispatch image is rebuilt from the context's current table snapshot (the defaults or the
  * last gpd_ctx_reload_tables), on its device; synchronous. */
 int  gpd_ctx_add_decoders(gpd_ctx *ctx, uint32_t decoders);
+/* ABI 8.  SetDecodingLayerContainer (parser.go:236-242): the registered set becomes exactly
+ * `decoders` (the kinds whose CanDecode types the container holds), replacing the previous set;
+ * rebuilt like gpd_ctx_add_decoders. */
+int  gpd_ctx_set_decoders(gpd_ctx *ctx, uint32_t decoders);
 int  gpd_ctx_destroy(gpd_ctx *ctx);
 /* Asynchronous on `stream` (a hipStream_t; NULL = the null stream).  Device pointers. */
 int  gpd_decode(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, void *stream);

@@ -368,6 +368,19 @@ static int check_reconfig(const gpd_config *base, const uint8_t *data, uint64_t 
     fprintf(stderr, "reconfig: no packet decoded VXLAN on the registered port\n");
     bad = 1;
   }
+  /* SetDecodingLayerContainer: the set replaced in place (VXLAN and Payload dropped) */
+  if (!bad) {
+    const uint32_t dec2 = base->decoders & ~(GPD_DEC_VXLAN | GPD_DEC_PAYLOAD);
+    CHECK(gpd_ctx_set_decoders(ctx, dec2));
+    gpd_batch hb = {data, data_len, off, cap, n};
+    gpd_result hr = {hv.status, hv.layers, hv.net_hash, hv.tp_hash, hv.csum, NULL, hv.hdr_off, NULL, hv.detail};
+    CHECK(gpd_decode_host(ctx, &hb, &hr));
+    gpo_decode_batch(data, off, cap, n, GPD_LT_ETHERNET, dec2, opts[2], &t, ov.status, ov.layers,
+                     ov.net_hash, ov.tp_hash, ov.csum, ov.hdr_off, oext, 8);
+    bad |= res_cmp("set_decoders host vs oracle", &hv, &ov, n);
+    if (!bad) bad |= detail_cmp("set_decoders detail", &hv, oext, n);
+    CHECK(gpd_ctx_set_decoders(ctx, base->decoders));
+  }
   /* a batch of empty packets (every CapLen 0, no data) */
   if (!bad) {
     const uint64_t m = 7;

@@ -556,6 +556,48 @@ def test_reconfigure_in_place_keeps_tables_and_context():
         L.TABLES.udp_port[:] = saved.udp_port
 
 
+def test_set_decoding_layer_container_in_place():
+    """SetDecodingLayerContainer (parser.go:236-242) replaces the registered decoders — fewer
+    here, then more — on the same gpd_ctx (gpd_ctx_set_decoders), and each set equals the oracle
+    with that mask; a DecodingLayerFunc (layers_decoder.go:11-101) from a Sparse container
+    returns the reference's (LayerType, error) pairs; DecodeLayers with no decoder for `first`
+    leaves the caller's decoded list as it was (layers_decoder.go:12-16)."""
+    from gopacket_amd import parser as P
+    pk = _golden_packets()
+    b = PacketBatch.from_packets(pk)
+    p = P.NewDecodingLayerParser(L.LayerTypeEthernet, *[P.DECODER_BY_NAME[k]() for k in P.DECODER_BY_NAME])
+    p.DecodeBatch(b)
+    h = p.ctx().h.value
+    small = P.DecodingLayerSparse()
+    for d in (P.Ethernet(), P.IPv4(), P.UDP(), P.Payload()):
+        small = small.Put(d)
+    arr = P.DecodingLayerArray()
+    for d in (P.Ethernet(), P.Dot1Q(), P.IPv6(), P.TCP(), P.VXLAN(), P.IPv4(), P.UDP()):
+        arr = arr.Put(d)
+    for dlc in (small, arr):
+        p.SetDecodingLayerContainer(dlc)
+        ref = O.decode(b, L.LayerTypeEthernet, p.decoders, 0, ext=True, nthreads=8)
+        for e in (False, True):
+            assert_same(p.DecodeBatch(b, ext=e), ref, b, e)
+        assert p.ctx().h.value == h, "the context was re-created"
+    fn = small.LayersDecoder(L.LayerTypeEthernet, p)
+    ref = O.decode(b, L.LayerTypeEthernet, small.engine_mask(), 0, ext=True, nthreads=8)
+    for i in range(0, len(pk), 3):
+        decoded = []
+        p.Truncated = False
+        typ, err = fn(pk[i], decoded)
+        st = int(ref.status[i]) & 3
+        assert decoded == ref.decoded(i), i
+        assert typ == (ref.stop_type(i) if st == 1 else 0), i
+        assert str(err) == str(ref.err(i) if st == 2 else None), i
+        assert p.Truncated == ref.truncated(i), i
+    q = P.NewDecodingLayerParser(L.LayerTypeIPv4, P.Ethernet(), P.TCP())  # nothing takes IPv4
+    decoded = [L.LayerTypeEthernet, L.LayerTypeTCP]
+    err = q.DecodeLayers(pk[0], decoded)
+    assert decoded == [L.LayerTypeEthernet, L.LayerTypeTCP]
+    assert str(err) == str(P.UnsupportedLayerType(L.LayerTypeIPv4))
+
+
 def test_all_empty_batch():
     """A batch whose every packet is empty (CapLen 0, data_len 0): Ethernet's "too small" error
     for each, on the device and host paths."""
