@@ -12,10 +12,10 @@ from . import layers
 from .layers import *  # noqa: F401,F403  LayerType constants, Register*PortLayerType
 from .batch import PacketBatch
 from .errors import DecodeError, UnsupportedLayerType
-from .results import BatchResult
+from .results import BatchResult, Endpoint, Flow
 
 __all__ = ["layers", "PacketBatch", "BatchResult", "DecodeError", "UnsupportedLayerType",
-           "parser"]
+           "Endpoint", "Flow", "parser"]
 
 
 def __getattr__(name):

@@ -54,6 +54,81 @@ def st_errcode(s):
     return (s >> 9) & 63
 
 
+# ---- Endpoint / Flow (flows.go, layers/endpoints.go:20-35) ----------------------------------
+EndpointIPv4, EndpointIPv6, EndpointTCPPort, EndpointUDPPort = 1, 2, 4, 5
+
+
+class Endpoint:
+    """flows.go:24-110: an endpoint type and its raw bytes (a view of the packet's)."""
+
+    def __init__(self, typ: int, raw: bytes):
+        self.typ, self.raw = int(typ), bytes(raw)
+
+    def EndpointType(self) -> int:
+        return self.typ
+
+    def Raw(self) -> bytes:
+        return self.raw
+
+    def String(self) -> str:  # layers/endpoints.go:41-95: net.IP / port formatting
+        if self.typ == EndpointIPv4:
+            return ".".join(str(b) for b in self.raw)
+        if self.typ == EndpointIPv6:
+            import ipaddress
+            return str(ipaddress.IPv6Address(self.raw))
+        if self.typ in (EndpointTCPPort, EndpointUDPPort):
+            return str(int.from_bytes(self.raw, "big"))
+        return self.raw.hex()
+
+    __str__ = String
+
+    def __eq__(self, o):
+        return isinstance(o, Endpoint) and (self.typ, self.raw) == (o.typ, o.raw)
+
+    def __hash__(self):
+        return hash((self.typ, self.raw))
+
+
+class Flow:
+    """flows.go:112-224: the two endpoints of one layer, in packet order.  A Flow from a
+    decoded batch (BatchResult.NetworkFlow / TransportFlow) carries the FastHash the kernel
+    computed for it; FastHash is symmetric (flows.go:159-174), so Reverse() keeps it."""
+
+    def __init__(self, typ: int, src: bytes, dst: bytes, fast_hash: Optional[int] = None):
+        self.typ, self.src, self.dst, self._hash = int(typ), bytes(src), bytes(dst), fast_hash
+
+    def EndpointType(self) -> int:
+        return self.typ
+
+    def Src(self) -> Endpoint:
+        return Endpoint(self.typ, self.src)
+
+    def Dst(self) -> Endpoint:
+        return Endpoint(self.typ, self.dst)
+
+    def Endpoints(self):
+        return self.Src(), self.Dst()
+
+    def Reverse(self) -> "Flow":
+        return Flow(self.typ, self.dst, self.src, self._hash)
+
+    def FastHash(self) -> int:
+        if self._hash is None:
+            raise ValueError("this Flow was not produced by a decode: its FastHash is the kernel's")
+        return self._hash
+
+    def String(self) -> str:  # flows.go:207-212
+        return f"{self.Src()}->{self.Dst()}"
+
+    __str__ = String
+
+    def __eq__(self, o):
+        return isinstance(o, Flow) and (self.typ, self.src, self.dst) == (o.typ, o.src, o.dst)
+
+    def __hash__(self):
+        return hash((self.typ, self.src, self.dst))
+
+
 @dataclass
 class BatchResult:
     status: np.ndarray            # uint32[n]
@@ -139,6 +214,27 @@ class BatchResult:
         """Offset of the layer TransportFlow() reads (the last TCP/UDP), or None."""
         h = int(self.hdr_off[i]) >> 16
         return None if h == 0xFFFF else h
+
+    def NetworkFlow(self, i: int, batch) -> Optional[Flow]:
+        """ip4/ip6.NetworkFlow() (ip4.go:63-65, ip6.go:49-51) of packet i as the call leaves the
+        object: its addresses read from the packet bytes at the header offset (zero copy from
+        `batch`, the PacketBatch decoded), its FastHash the kernel's.  None without one."""
+        s = int(self.status[i])
+        ept, off = (s >> 20) & 15, self.network_offset(i)
+        if ept == 0 or off is None:
+            return None
+        p = batch.packet(i)
+        a, n = (12, 4) if ept == EndpointIPv4 else (8, 16)
+        return Flow(ept, p[off + a:off + a + n], p[off + a + n:off + a + 2 * n], self.network_flow_hash(i))
+
+    def TransportFlow(self, i: int, batch) -> Optional[Flow]:
+        """tcp/udp.TransportFlow() (tcp.go:331-333, udp.go:123-125): the ports, as above."""
+        s = int(self.status[i])
+        ept, off = (s >> 24) & 15, self.transport_offset(i)
+        if ept == 0 or off is None:
+            return None
+        p = batch.packet(i)
+        return Flow(ept, p[off:off + 2], p[off + 2:off + 4], self.transport_flow_hash(i))
 
     def layer(self, i: int, name: str):
         """(contents, payload) byte ranges of a layer object after the call, or None."""

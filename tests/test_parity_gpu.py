@@ -598,6 +598,45 @@ def test_set_decoding_layer_container_in_place():
     assert str(err) == str(P.UnsupportedLayerType(L.LayerTypeIPv4))
 
 
+def test_flows_from_results():
+    """NetworkFlow() / TransportFlow() rebuilt from the result words and the packet bytes
+    (gopacket_amd.results.Flow): testSimpleTCPPacket's endpoints as decode_test.go:404-405,430-431
+    asserts them ("172.17.81.73" -> "173.222.254.225", "50679" -> "80"); over the mixed batch
+    (IPv4, IPv6, VXLAN inner flows) each Flow's endpoints are the bytes at the oracle's header
+    offsets, its FastHash the oracle's, and Reverse() keeps it (doc.go:216-219)."""
+    from gopacket_amd import parser as P
+    from gopacket_amd.results import EndpointIPv4, EndpointTCPPort
+    c = next(c for c in CASES if c["name"] == "simple_tcp_full")
+    b = G.single_batch(c)
+    first, mask, opts = G.case_config(c)
+    res = _parser(first, mask, opts).DecodeBatch(b)
+    nf, tf = res.NetworkFlow(0, b), res.TransportFlow(0, b)
+    assert nf.EndpointType() == EndpointIPv4 and tf.EndpointType() == EndpointTCPPort
+    assert (str(nf.Src()), str(nf.Dst())) == ("172.17.81.73", "173.222.254.225")
+    assert (str(tf.Src()), str(tf.Dst())) == ("50679", "80")
+    assert nf.String() == "172.17.81.73->173.222.254.225"
+    mb = synth.make_mixed(3000)
+    p = P.NewDecodingLayerParser(L.LayerTypeEthernet, *[P.DECODER_BY_NAME[k]() for k in P.DECODER_BY_NAME])
+    dev = p.DecodeBatch(mb)
+    ref = O.decode(mb, L.LayerTypeEthernet, p.decoders, 0, ext=False, nthreads=8)
+    seen = set()
+    for i in range(mb.n):
+        pk = mb.packet(i)
+        for f, h, off in ((dev.NetworkFlow(i, mb), ref.network_flow_hash(i), ref.network_offset(i)),
+                          (dev.TransportFlow(i, mb), ref.transport_flow_hash(i), ref.transport_offset(i))):
+            if h is None:
+                assert f is None or off is not None
+                continue
+            assert f is not None and f.FastHash() == h and f.Reverse().FastHash() == h
+            seen.add(f.EndpointType())
+            if f.EndpointType() in (1, 2):
+                a, n = (12, 4) if f.EndpointType() == 1 else (8, 16)
+                assert f.src == pk[off + a:off + a + n] and f.dst == pk[off + a + n:off + a + 2 * n]
+            else:
+                assert f.src == pk[off:off + 2] and f.dst == pk[off + 2:off + 4]
+    assert seen >= {1, 4, 5}
+
+
 def test_all_empty_batch():
     """A batch whose every packet is empty (CapLen 0, data_len 0): Ethernet's "too small" error
     for each, on the device and host paths."""
