@@ -75,9 +75,10 @@ struct KParams {
   uint32_t nstores;            // store instructions per tile (non-NULL result arrays)
   uint32_t fixed;              // tables in the kFix* layout (eth_mult shared by all three)
   uint32_t waves;              // fast kernel waves per SIMD (0: the default for the window)
-  uint32_t *fb_list;           // fast kernel: packet indices left to the generic decoder, in one
-                               // private region per wave (64 x its tiles), which that wave
-                               // decodes after its tiles (see rs_kernel)
+  uint64_t *fb_list;           // fast kernel: packets left to the generic decoder (offset << 32 |
+                               // index: the decode's loads skip the descriptor), in one private
+                               // region per wave (64 x its tiles), which that wave decodes after
+                               // its tiles (see rs_kernel)
   uint32_t *fb_wcount;         // per fast-kernel wave: entries in its region
   uint32_t fb_waves;           // waves of the fast launch (set by launch_decode)
 };

@@ -669,13 +669,13 @@ static int launch(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, hipS
         fb.cap = 0;
       }
       // the list: 64 entries per tile (each wave's region spans its tiles), after the flags
-      HIP_TRY(hipMalloc(&fb.d, (need + 64 + 128) * sizeof(uint32_t)));
+      HIP_TRY(hipMalloc(&fb.d, 128 * sizeof(uint32_t) + (need + 64) * sizeof(uint64_t)));
       HIP_TRY(hipMemset(fb.d, 0, 128 * sizeof(uint32_t)));  // both flags start at zero
       HIP_TRY(hipMalloc(&fb.wc, 2ull * ctx->num_cus * gpd::kMaxFastWavesPerCU * sizeof(uint32_t)));
       fb.cap = need;
       fb.parity = 0;
     }
-    P.fb_list = fb.d + 128;
+    P.fb_list = reinterpret_cast<uint64_t *>(fb.d + 128);
   }
   if (record) HIP_TRY(hipEventRecord(ctx->ev0, stream));
   const bool split = record && in->n <= gpd::kMaxLaunchPackets && gpd::fast_eligible(P);
