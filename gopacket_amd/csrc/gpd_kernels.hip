@@ -1753,14 +1753,11 @@ __global__ __launch_bounds__(64 * WAVES, MINW) void decode_kernel(KParams P) {
 // memory.
 template <uint32_t K, bool CS = true, bool HASH = true>
 __device__ __forceinline__ void decode_fallback_list(const KParams &P, uint32_t buf, uint32_t fb_start, uint32_t fb_c,
-                                                     uint32_t lane, uint32_t dlen, uint32_t options,
-                                                     uint32_t fb_end = 0, uint32_t fb_v = 0) {
+                                                     uint32_t lane, uint32_t dlen, uint32_t options) {
 #if GPD_EXP & 8
   return;  // (A/B diagnostic build, tools/mix_diag.sh: the generic decodes skipped, wrong results)
 #endif
-  // entries [fb_start, fb_start + fb_c), then the fb_v stored downward from fb_end (ro_kernel's
-  // VXLAN frames: decoded after the rest, so that the rounds holding them run no other stack)
-  const uint32_t tot = fb_c + fb_v;
+  const uint32_t tot = fb_c;
   if (tot) {
     __threadfence_block();  // the entries other lanes of this wave stored
     const Tab<false> T{P.pages,    P.eth_base, P.tcp_base, P.udp_base, P.eth_bits,
@@ -1778,7 +1775,7 @@ __device__ __forceinline__ void decode_fallback_list(const KParams &P, uint32_t 
     };
     auto fetch = [&](uint32_t j, Fetch &f) {
       const bool live = j < tot;
-      const uint64_t e = live ? P.fb_list[j < fb_c ? fb_start + j : fb_end - 1u - (j - fb_c)] : 0ull;
+      const uint64_t e = live ? P.fb_list[fb_start + j] : 0ull;
       f.fi = (uint32_t)e;
       f.off = (uint32_t)(e >> 32);  // (clamped to dlen when listed)
       f.len = live ? min(P.caplen[f.fi], dlen - f.off) : 0u;
@@ -1923,9 +1920,7 @@ __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
   // every tile, serialised at the memory side); the wave decodes its region after its tiles.
   const uint32_t gw = tp;
   const uint32_t fb_start = 64u * (gw * (ntiles / nwaves) + min(gw, ntiles % nwaves));
-  // the region's end: 64 entries per tile this wave owns; VXLAN frames are listed downward from it
-  const uint32_t fb_end = fb_start + 64u * (ntiles / nwaves + (gw < ntiles % nwaves ? 1u : 0u));
-  uint32_t fb_c = 0, fb_v = 0;
+  uint32_t fb_c = 0;
   if (tp >= ntiles) {
     if (lane == 0u) P.fb_wcount[gw] = 0u;
     return;
@@ -2239,9 +2234,7 @@ __global__ __launch_bounds__(256, MINW) void ro_kernel(KParams P) {
   uint32_t tp = blockIdx.x * WAVES + wave;  // the planner's tile
   const uint32_t gw = tp;  // this wave's fallback region (see rs_kernel)
   const uint32_t fb_start = 64u * (gw * (ntiles / nwaves) + min(gw, ntiles % nwaves));
-  // the region's end: 64 entries per tile this wave owns; VXLAN frames are listed downward from it
-  const uint32_t fb_end = fb_start + 64u * (ntiles / nwaves + (gw < ntiles % nwaves ? 1u : 0u));
-  uint32_t fb_c = 0, fb_v = 0;
+  uint32_t fb_c = 0;
   if (tp >= ntiles) {
     if (lane == 0u) P.fb_wcount[gw] = 0u;
     return;
@@ -2270,16 +2263,6 @@ __global__ __launch_bounds__(256, MINW) void ro_kernel(KParams P) {
       fb_c += (uint32_t)__popcll(m);
     }
   };
-#if GPD_EXP & 16
-  auto fb_append_vx = [&](uint32_t i, uint32_t off, uint32_t fb) {  // VXLAN frames: from the region's end down
-    const uint64_t m = __ballot(fb != 0);
-    if (m) {
-      if (fb) P.fb_list[fb_end - 1u - fb_v - __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = ((uint64_t)off << 32) | i;
-      fb_v += (uint32_t)__popcll(m);
-    }
-  };
-#endif
   // A tile's byte run [t0, t0 + 8192 nr): its packets' extent, in nr rounds; nr = 0 when the
   // packets are not nearly back to back (or hold no bytes): the tile goes to the fallback list.
   uint32_t t0_p = 0, t1_p = 0, nr_p = 0;
@@ -2444,13 +2427,7 @@ __global__ __launch_bounds__(256, MINW) void ro_kernel(KParams P) {
         }
         const uint32_t i = td * 64u + lane;
         const uint32_t valid = (ls & kValid) ? 1u : 0u;
-#if !(GPD_EXP & 16)
         fb_append(i, off_d, valid ? fb : 0u);
-#else
-        const uint32_t vx = (ls & (kStaged | kFb)) == (kStaged | kFb) ? 1u : 0u;
-        fb_append(i, off_d, valid && !vx ? fb : 0u);
-        fb_append_vx(i, off_d, valid & vx);
-#endif
         if (valid && !fb) store_out(P, i, res);
       }
       if (!has_next) break;
@@ -2468,8 +2445,8 @@ __global__ __launch_bounds__(256, MINW) void ro_kernel(KParams P) {
       }
     }
   }
-  if (lane == 0u) P.fb_wcount[gw] = fb_c + fb_v;  // (gpd_last_launch_split's count)
-  decode_fallback_list<kRoStage / 64u, CS, HASH>(P, buf, fb_start, fb_c, lane, dlen, options, fb_end, fb_v);
+  if (lane == 0u) P.fb_wcount[gw] = fb_c;  // (gpd_last_launch_split's count)
+  decode_fallback_list<kRoStage / 64u, CS, HASH>(P, buf, fb_start, fb_c, lane, dlen, options);
 }
 
 template <int STAGE, bool FAST, bool EXT, bool PAGES, bool SWZ, int WAVES, bool CS = true,
