@@ -1757,6 +1757,12 @@ __device__ __forceinline__ void decode_fallback_list(const KParams &P, uint32_t 
 #if GPD_EXP & 8
   return;  // (A/B diagnostic build, tools/mix_diag.sh: the generic decodes skipped, wrong results)
 #endif
+#if GPD_EXP & 64
+  options |= GPD_OPT_NO_FLOW_HASH;  // (A/B diagnostic: the generic decodes' hashes skipped)
+#endif
+#if GPD_EXP & 128
+  options |= GPD_OPT_NO_CHECKSUMS;  // (A/B diagnostic: the generic decodes' checksums skipped)
+#endif
   const uint32_t tot = fb_c;
   if (tot) {
     __threadfence_block();  // the entries other lanes of this wave stored
