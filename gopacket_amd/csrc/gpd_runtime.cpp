@@ -245,7 +245,9 @@ struct gpd_ctx {
     gpd_detail *h_det = nullptr, *d_det = nullptr;
     uint32_t *d_pw = nullptr;  // the device pcap walk's per-segment arrays (5 x kPwMaxSeg)
     uint8_t *d_tw = nullptr, *h_tw = nullptr;  // the device TPACKET_V3 walk's tables + results
-    hipStream_t stream_out = nullptr;          // its D2H (gpd_decode_tpv3)
+    hipStream_t stream_out = nullptr;          // its D2H (gpd_decode_tpv3, gpd_decode_host)
+    // gpd_decode_host: the chunk's H2D done (host staging reusable), decoded, results back
+    hipEvent_t ev_in = nullptr, ev_dec = nullptr, ev_out = nullptr;
     uint64_t lo = 0, hi = 0;  // packet range in flight
     bool busy = false;
     bool direct = false;      // its results go straight into the caller's (registered) arrays
@@ -476,6 +478,8 @@ static void free_slots(gpd_ctx *ctx) {
       if (p) (void)hipFree(p);
     if (s.stream) (void)hipStreamDestroy(s.stream);
     if (s.stream_out) (void)hipStreamDestroy(s.stream_out);
+    for (hipEvent_t e : {s.ev_in, s.ev_dec, s.ev_out})
+      if (e) (void)hipEventDestroy(e);
     s = gpd_ctx::Slot{};
   }
   if (ctx->d_pw_ctl) (void)hipFree(ctx->d_pw_ctl);
@@ -868,7 +872,7 @@ static void drain_slot(gpd_ctx::Slot &s, const gpd_result *out) {
 // caller's arrays when every one of them lies in registered memory (gpd_host_register; then
 // the drain copies nothing), else into the slot's pinned arrays for drain_slot to copy.
 static hipError_t results_d2h(gpd_ctx *ctx, gpd_ctx::Slot &s, const gpd_result *out, uint64_t lo,
-                              uint64_t m) {
+                              uint64_t m, hipStream_t stream) {
   auto reg = [&](const void *p, uint64_t bytes) {
     return p == nullptr || ctx->is_registered(static_cast<const uint8_t *>(p), bytes);
   };
@@ -879,7 +883,7 @@ static hipError_t results_d2h(gpd_ctx *ctx, gpd_ctx::Slot &s, const gpd_result *
              reg(out->hdr_off ? out->hdr_off + lo : nullptr, m * 4) &&
              reg(out->detail ? out->detail + lo : nullptr, m * sizeof(gpd_detail));
   auto cp = [&](void *host, const void *dev, uint64_t bytes) {
-    return hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, s.stream);
+    return hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, stream);
   };
   hipError_t e = cp(s.direct ? (void *)(out->status + lo) : (void *)s.h_status, s.d_status, m * 4);
   if (e == hipSuccess) e = cp(s.direct ? (void *)(out->layers + lo) : (void *)s.h_layers, s.d_layers, m * 8);
@@ -908,15 +912,19 @@ int gpd_decode_host(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out) {
   const uint64_t kPkts = 1u << 20, kBytes = 256ull << 20;
   int rc = alloc_slots(ctx, kBytes, kPkts, out->ext != nullptr, out->detail != nullptr);
   if (rc) return rc;
+  // Each slot's chunk: H2D and decode on its stream, the results D2H on its stream_out, so the
+  // next chunks' H2D never waits behind a D2H (the link carries both directions at once)
+  for (auto &s : ctx->slot) {
+    if (!s.stream_out) HIP_TRY(hipStreamCreateWithFlags(&s.stream_out, hipStreamNonBlocking));
+    for (hipEvent_t *e : {&s.ev_in, &s.ev_dec, &s.ev_out})
+      if (!*e) HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  }
   SlotGuard guard{ctx};
   uint64_t i = 0;
   int k = 0;
   while (i < in->n) {
     auto &s = ctx->slot[k];
-    if (s.busy) {
-      HIP_TRY(hipStreamSynchronize(s.stream));
-      drain_slot(s, out);
-    }
+    if (s.busy) HIP_TRY(hipEventSynchronize(s.ev_in));  // chunk k-2's H2D read the host staging
     // Span mode: packets [i, j) lie inside one window of the source buffer of at most kBytes
     // with few gaps (the usual back-to-back batch): that window travels as it is (straight
     // from the caller's buffer when it is registered) and the offsets are rebased.
@@ -986,6 +994,11 @@ int gpd_decode_host(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out) {
     const uint64_t m = j - i;
     HIP_TRY(hipMemcpyAsync(s.d_off, dreg ? in->offset + i : s.h_off, m * 4, hipMemcpyHostToDevice, s.stream));
     HIP_TRY(hipMemcpyAsync(s.d_len, dreg ? in->caplen + i : s.h_len, m * 4, hipMemcpyHostToDevice, s.stream));
+    HIP_TRY(hipEventRecord(s.ev_in, s.stream));
+    if (s.busy) {  // chunk k-2's results are back (and drained) before this decode rewrites them
+      HIP_TRY(hipEventSynchronize(s.ev_out));
+      drain_slot(s, out);
+    }
     gpd_batch b{s.d_data, pos, s.d_off, s.d_len, m};
     if (dreg) {
       b.data = s.d_data - lo16;  // 16-aligned (lo16 is); the kernel never reads below lo16
@@ -995,7 +1008,10 @@ int gpd_decode_host(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out) {
                  out->hdr_off ? s.d_hoff : nullptr, nullptr, out->detail ? s.d_det : nullptr};
     rc = launch(ctx, &b, &r, s.stream, false, nullptr, 0, pos);
     if (rc) return rc;
-    HIP_TRY(results_d2h(ctx, s, out, i, m));
+    HIP_TRY(hipEventRecord(s.ev_dec, s.stream));
+    HIP_TRY(hipStreamWaitEvent(s.stream_out, s.ev_dec, 0));
+    HIP_TRY(results_d2h(ctx, s, out, i, m, s.stream_out));
+    HIP_TRY(hipEventRecord(s.ev_out, s.stream_out));
     s.lo = i;
     s.hi = j;
     s.busy = true;
@@ -1005,6 +1021,7 @@ int gpd_decode_host(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out) {
   for (auto &s : ctx->slot) {
     if (s.busy) {
       HIP_TRY(hipStreamSynchronize(s.stream));
+      HIP_TRY(hipStreamSynchronize(s.stream_out));
       drain_slot(s, out);
     }
   }
@@ -1220,7 +1237,7 @@ static int decode_pcap_host_walk(gpd_ctx *ctx, const uint8_t *buf, uint64_t len,
                    out->hdr_off ? s.d_hoff : nullptr, nullptr, out->detail ? s.d_det : nullptr};
       rc = launch(ctx, &b, &r, s.stream, false);
       if (rc) return rc;
-      e = results_d2h(ctx, s, out, done + i, m);
+      e = results_d2h(ctx, s, out, done + i, m, s.stream);
       if (e != hipSuccess) {
         return set_err(GPD_ERR_HIP, "gpd_decode_pcap: D2H: %s", hipGetErrorString(e));
       }
@@ -1387,7 +1404,7 @@ static int decode_device_walk(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, co
       break;
     }
     const uint64_t take = std::min<uint64_t>(c.n, max_n - done);
-    hipError_t e = results_d2h(ctx, s, out, done, take);
+    hipError_t e = results_d2h(ctx, s, out, done, take, s.stream);
     if (e != hipSuccess) return set_err(GPD_ERR_HIP, "gpd_decode_pcap: D2H: %s", hipGetErrorString(e));
     s.lo = done;
     s.hi = done + take;
