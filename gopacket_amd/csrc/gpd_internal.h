@@ -120,7 +120,10 @@ hipError_t launch_pcap_fill(const PwArgs &A, hipStream_t stream);
 // The TPACKET_V3 block walk on the GPU (gpd_tpv3walk.hip): one group of consecutive ring
 // blocks in HBM, one workgroup per block.
 constexpr uint32_t kTwWin = 32768;           // LDS window of a block's bytes
-constexpr uint64_t kTwGroup = 64ull << 20;   // bytes of ring blocks per group
+#ifndef GPD_TW_GROUP_MIB
+#define GPD_TW_GROUP_MIB 64  // (A/B builds override it)
+#endif
+constexpr uint64_t kTwGroup = (uint64_t)GPD_TW_GROUP_MIB << 20;  // bytes of ring blocks per group
 struct TwBlock {      // one walked block (host plan, afpacket.go:303-316 + header.go:144-149)
   uint32_t entry;     // its first emitted packet header (relative to the block; 16-aligned)
   uint32_t emit;      // packets the read loop returns from it
