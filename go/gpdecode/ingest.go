@@ -408,3 +408,55 @@ func (r *Result) truncate(n int) {
 	r.TpHash, r.Checksum, r.HdrOff = r.TpHash[:n], r.Checksum[:n], r.HdrOff[:n]
 	r.Detail = r.Detail[:n]
 }
+
+// FastHashes is Flow.FastHash (flows.go:167-174) of many caller-built flows in one device
+// launch (gpd_fast_hash): the EndpointType, both raw endpoints zero-padded to
+// gopacket.MaxEndpointSize and their lengths go to HBM as gopacket lays a Flow out, and
+// out[i] == flows[i].FastHash().  Use it for keys a program builds itself (tcpassembly's
+// [2]gopacket.Flow from stored records); decoded packets carry theirs in Result.NetHash/TpHash.
+func (p *BatchDecodingLayerParser) FastHashes(flows []gopacket.Flow) ([]uint64, error) {
+	n := len(flows)
+	out := make([]uint64, n)
+	if n == 0 {
+		return out, nil
+	}
+	typ := make([]int64, n)
+	raw := make([]byte, 32*n) // src rows, then dst rows, 16 bytes each
+	lens := make([]byte, 2*n) // src lengths, then dst lengths
+	for i, f := range flows {
+		src, dst := f.Endpoints()
+		typ[i] = int64(f.EndpointType())
+		lens[i] = byte(copy(raw[16*i:16*i+16], src.Raw()))
+		lens[n+i] = byte(copy(raw[16*(n+i):16*(n+i)+16], dst.Raw()))
+	}
+	done, err := p.onDevice()
+	if err != nil {
+		return nil, err
+	}
+	defer done()
+	sizes := []int{8 * n, 32 * n, 2 * n, 8 * n}
+	bufs := make([]devBuf, len(sizes))
+	for k, s := range sizes {
+		d, err := devAlloc(s)
+		if err != nil {
+			return nil, err
+		}
+		bufs[k] = d
+		defer d.free()
+	}
+	for k, h := range []unsafe.Pointer{unsafe.Pointer(&typ[0]), unsafe.Pointer(&raw[0]), unsafe.Pointer(&lens[0])} {
+		if err := toDev(bufs[k], h, sizes[k]); err != nil {
+			return nil, err
+		}
+	}
+	src := (*C.uint8_t)(bufs[1].p)
+	dst := (*C.uint8_t)(unsafe.Add(bufs[1].p, 16*n))
+	if rc := C.gpd_fast_hash(C.int(p.device), C.uint64_t(n), (*C.int64_t)(bufs[0].p), src, (*C.uint8_t)(bufs[2].p),
+		dst, (*C.uint8_t)(unsafe.Add(bufs[2].p, n)), (*C.uint64_t)(bufs[3].p), nil); rc != C.GPD_OK {
+		return nil, lastError("gpd_fast_hash", rc)
+	}
+	if e := C.hipMemcpy(unsafe.Pointer(&out[0]), bufs[3].p, C.size_t(8*n), C.hipMemcpyDeviceToHost); e != C.hipSuccess {
+		return nil, errors.New(C.GoString(C.hipGetErrorString(e)))
+	}
+	return out, nil
+}

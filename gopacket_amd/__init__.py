@@ -12,10 +12,12 @@ from . import layers
 from .layers import *  # noqa: F401,F403  LayerType constants, Register*PortLayerType
 from .batch import PacketBatch
 from .errors import DecodeError, UnsupportedLayerType
-from .results import BatchResult, Endpoint, Flow
+from .results import (BatchResult, Endpoint, FastHashes, Flow, FlowFromEndpoints, MaxEndpointSize,
+                      NewEndpoint, NewFlow)
 
 __all__ = ["layers", "PacketBatch", "BatchResult", "DecodeError", "UnsupportedLayerType",
-           "Endpoint", "Flow", "parser"]
+           "Endpoint", "Flow", "NewEndpoint", "NewFlow", "FlowFromEndpoints", "FastHashes",
+           "MaxEndpointSize", "parser"]
 
 
 def __getattr__(name):

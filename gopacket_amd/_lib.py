@@ -11,7 +11,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libgpd.so")
 
-GPD_ABI_VERSION = 8
+GPD_ABI_VERSION = 9
 GPD_OK = 0
 GPD_ERR_INVALID = -1
 
@@ -96,6 +96,8 @@ EXPORTS = {
     "gpd_flow_export": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
                                   C.POINTER(C.c_uint64), C.c_void_p]),
     "gpd_flow_destroy": (C.c_int, [C.c_void_p]),
+    "gpd_fast_hash": (C.c_int, [C.c_int, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                C.c_void_p, C.c_void_p, C.c_void_p]),
     "gpd_flow_test_fingerprint_bits": (C.c_int, [C.c_void_p, C.c_uint32]),
     "gpd_flow_test_counter_bits": (C.c_int, [C.c_void_p, C.c_uint32]),
     "gpd_flow_keys": (C.c_int, [C.c_void_p, C.POINTER(GpdBatch), C.POINTER(GpdResult), C.c_uint32,

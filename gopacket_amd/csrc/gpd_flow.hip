@@ -625,7 +625,44 @@ static hipError_t grow_made(gpd_flowtable *ft, uint64_t n) {
   return e;
 }
 
+// Endpoint / Flow FastHash of caller-built keys (gpd_fast_hash): one lane per key.
+__device__ __forceinline__ uint64_t fnv_raw16(uint4 raw, uint32_t len) {  // flows.go:60-67
+  const uint32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
+  uint64_t h = 14695981039346656037ull;
+#pragma unroll
+  for (uint32_t k = 0; k < 16; k++)
+    if (k < len) h = (h ^ ((w[k >> 2] >> (8 * (k & 3))) & 0xFFu)) * 1099511628211ull;
+  return h;
+}
+__global__ __launch_bounds__(256) void fast_hash_kernel(uint64_t n, const int64_t *typ, const uint4 *src,
+                                                        const uint8_t *src_len, const uint4 *dst,
+                                                        const uint8_t *dst_len, uint64_t *out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t h = fnv_raw16(src[i], src_len[i]);
+    if (dst) h += fnv_raw16(dst[i], dst_len[i]);  // flows.go:170: commutative in src and dst
+    out[i] = (h ^ (uint64_t)typ[i]) * 1099511628211ull;
+  }
+}
+
 extern "C" {
+
+int gpd_fast_hash(int device, uint64_t n, const int64_t *typ, const uint8_t *src, const uint8_t *src_len,
+                  const uint8_t *dst, const uint8_t *dst_len, uint64_t *out, void *stream) {
+  if (n == 0) return GPD_OK;
+  if (!typ || !src || !src_len || !out || (dst && !dst_len))
+    return gpd::set_error(GPD_ERR_INVALID, "gpd_fast_hash: null argument");
+  if (((uintptr_t)src | (uintptr_t)(dst ? dst : src)) & 15u)
+    return gpd::set_error(GPD_ERR_INVALID, "gpd_fast_hash: raw arrays must be 16-byte aligned");
+  FLOW_TRY(hipSetDevice(device));
+  int cus = 0;
+  FLOW_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+  const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, (uint64_t)std::max(cus, 1) * 8);
+  hipLaunchKernelGGL(fast_hash_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, n, typ,
+                     reinterpret_cast<const uint4 *>(src), src_len, reinterpret_cast<const uint4 *>(dst),
+                     dst_len, out);
+  FLOW_TRY(hipGetLastError());
+  return GPD_OK;
+}
 
 int gpd_flow_create(gpd_ctx *ctx, uint64_t capacity, gpd_flowtable **out) {
   if (!ctx || !out) return gpd::set_error(GPD_ERR_INVALID, "gpd_flow_create: null argument");

@@ -56,6 +56,48 @@ def st_errcode(s):
 
 # ---- Endpoint / Flow (flows.go, layers/endpoints.go:20-35) ----------------------------------
 EndpointIPv4, EndpointIPv6, EndpointTCPPort, EndpointUDPPort = 1, 2, 4, 5
+MaxEndpointSize = 16  # flows.go:27
+
+
+def _device_fast_hash(typs, srcs, dsts=None, device: Optional[int] = None) -> np.ndarray:
+    """FastHash of n endpoints (dsts None) or flows on the GPU (gpd_fast_hash, flows.go:60-83,
+    167-174): the raw bytes zero-padded to 16 as gopacket keeps them."""
+    import torch
+    from ._lib import check, lib
+    if not torch.cuda.is_available():
+        raise RuntimeError("FastHash of a caller-built Endpoint/Flow runs on the GPU (gpd_fast_hash); no GPU")
+    n = len(typs)
+    dev = torch.cuda.current_device() if device is None else int(device)
+
+    def pack(raws):
+        a = np.zeros((max(n, 1), 16), np.uint8)
+        ln = np.zeros(max(n, 1), np.uint8)
+        for i, r in enumerate(raws):
+            a[i, :len(r)] = np.frombuffer(r, np.uint8)
+            ln[i] = len(r)
+        return torch.from_numpy(a).to(dev), torch.from_numpy(ln).to(dev)
+    t = torch.from_numpy(np.asarray(typs, np.int64).reshape(-1)).to(dev)
+    s, sl = pack(srcs)
+    d, dl = pack(dsts) if dsts is not None else (None, None)
+    out = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    check(lib.gpd_fast_hash(dev, n, t.data_ptr(), s.data_ptr(), sl.data_ptr(),
+                            d.data_ptr() if d is not None else None, dl.data_ptr() if dl is not None else None,
+                            out.data_ptr(), stream.cuda_stream), "gpd_fast_hash")
+    stream.synchronize()
+    return out.cpu().numpy().view(np.uint64)[:n]
+
+
+def FastHashes(objs, device: Optional[int] = None) -> np.ndarray:
+    """FastHash of many Endpoints or many Flows in one device launch (uint64[n])."""
+    objs = list(objs)
+    if not objs:
+        return np.zeros(0, np.uint64)
+    if all(isinstance(o, Flow) for o in objs):
+        return _device_fast_hash([o.typ for o in objs], [o.src for o in objs], [o.dst for o in objs], device)
+    if all(isinstance(o, Endpoint) for o in objs):
+        return _device_fast_hash([o.typ for o in objs], [o.raw for o in objs], None, device)
+    raise TypeError("FastHashes: all Endpoints or all Flows")
 
 
 class Endpoint:
@@ -69,6 +111,12 @@ class Endpoint:
 
     def Raw(self) -> bytes:
         return self.raw
+
+    def LessThan(self, b: "Endpoint") -> bool:  # flows.go:53-55
+        return self.typ < b.typ or (self.typ == b.typ and self.raw < b.raw)
+
+    def FastHash(self) -> int:  # flows.go:78-83 (on the GPU: gpd_fast_hash)
+        return int(_device_fast_hash([self.typ], [self.raw])[0])
 
     def String(self) -> str:  # layers/endpoints.go:41-95: net.IP / port formatting
         if self.typ == EndpointIPv4:
@@ -112,9 +160,9 @@ class Flow:
     def Reverse(self) -> "Flow":
         return Flow(self.typ, self.dst, self.src, self._hash)
 
-    def FastHash(self) -> int:
-        if self._hash is None:
-            raise ValueError("this Flow was not produced by a decode: its FastHash is the kernel's")
+    def FastHash(self) -> int:  # flows.go:167-174
+        if self._hash is None:  # a caller-built flow: one gpd_fast_hash launch (FastHashes batches)
+            self._hash = int(_device_fast_hash([self.typ], [self.src], [self.dst])[0])
         return self._hash
 
     def String(self) -> str:  # flows.go:207-212
@@ -127,6 +175,27 @@ class Flow:
 
     def __hash__(self):
         return hash((self.typ, self.src, self.dst))
+
+
+def NewEndpoint(typ: int, raw: bytes) -> Endpoint:
+    """flows.go:89-97 (a raw longer than MaxEndpointSize panics there: ValueError here)."""
+    if len(raw) > MaxEndpointSize:
+        raise ValueError("raw byte length greater than MaxEndpointSize")
+    return Endpoint(typ, raw)
+
+
+def NewFlow(typ: int, src: bytes, dst: bytes) -> Flow:
+    """flows.go:214-224."""
+    if len(src) > MaxEndpointSize or len(dst) > MaxEndpointSize:
+        raise ValueError("flow raw byte length greater than MaxEndpointSize")
+    return Flow(typ, src, dst)
+
+
+def FlowFromEndpoints(src: Endpoint, dst: Endpoint):
+    """flows.go:151-157: (Flow, None), or (an empty Flow, the error) for mismatched types."""
+    if src.typ != dst.typ:
+        return Flow(0, b"", b""), ValueError(f"Mismatched endpoint types: {src.typ}->{dst.typ}")
+    return Flow(src.typ, src.raw, dst.raw), None
 
 
 @dataclass

@@ -50,13 +50,14 @@
 extern "C" {
 #endif
 
-#define GPD_ABI_VERSION 8  /* 2: ICMPv4 + LLC, 12 objects, 224-B ext; 3: gpd_result.hdr_off;
+#define GPD_ABI_VERSION 9  /* 2: ICMPv4 + LLC, 12 objects, 224-B ext; 3: gpd_result.hdr_off;
                               4: gpd_ctx_set_tuning; 5: gpd_tuning.header_once,
                               gpd_tuning.device_walk, gpd_result.records; 6: outputs follow the
                               objects as a failing call leaves them; ext err_obj/err_wrote/err_off;
                               7: gpd_result.detail (error arguments and deep stacks without ext);
                               8: gpd_ctx_set_options, gpd_ctx_add_decoders, gpd_ctx_set_decoders
-                              (in place: device, tables and staging kept) */
+                              (in place: device, tables and staging kept); 9: gpd_fast_hash
+                              (gpd_flow.h) */
 
 /* ---- gopacket LayerType numbers (layertypes.go:14-154, decode.go:105-116) ---- */
 #define GPD_LT_ZERO            0

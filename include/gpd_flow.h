@@ -94,6 +94,19 @@ int gpd_flow_stats_get(gpd_flowtable *ft, gpd_flow_stats *out, void *stream);
 int gpd_flow_export(gpd_flowtable *ft, gpd_flow_rec *out, uint32_t *rec_index, uint64_t max,
                     uint64_t *n, void *stream);
 int gpd_flow_destroy(gpd_flowtable *ft);
+
+/* Endpoint.FastHash / Flow.FastHash (flows.go:60-83,167-174) of n endpoints or flows held in
+ * device memory on `device` as gopacket lays them out (flows.go:32-36,142-146): typ[i] (the
+ * EndpointType, int64), the raw bytes zero-padded to MaxEndpointSize = 16 (src, dst: n x 16
+ * bytes, 16-byte aligned) and their lengths (src_len, dst_len: n bytes, at most 16, as
+ * NewEndpoint / NewFlow guarantee; larger values hash 16 bytes).  A flow (dst != NULL):
+ * out[i] = ((fnvHash(src) + fnvHash(dst)) ^ typ) * fnvPrime, the same for a flow and its
+ * Reverse(); an endpoint (dst == NULL, dst_len ignored): out[i] = (fnvHash(src) ^ typ) *
+ * fnvPrime.  Replaces the per-object methods for keys a caller builds itself (e.g. the
+ * [2]Flow keys of tcpassembly/assembly.go:289 from stored records). */
+int gpd_fast_hash(int device, uint64_t n, const int64_t *typ, const uint8_t *src, const uint8_t *src_len,
+                  const uint8_t *dst, const uint8_t *dst_len, uint64_t *out, void *stream);
+
 /* Testing hook: keep only the low `bits` (1..64) bits of every key fingerprint (56 or more =
  * all 56, the default) from the next insert on, so that distinct keys share fingerprints and the
  * collision path (GPD_FLOW_COLLISION, gpd_flow_stats.collisions) runs.  Call it on an empty

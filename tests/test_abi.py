@@ -39,7 +39,7 @@ def test_library_exports_every_declared_symbol():
     lib = C.CDLL(_lib.LIB_PATH)
     missing = [f for f in declared_functions() if not hasattr(lib, f)]
     assert not missing, missing
-    assert lib.gpd_abi_version() == 8
+    assert lib.gpd_abi_version() == 9
 
 
 def test_python_binding_covers_the_header():

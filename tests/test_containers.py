@@ -44,3 +44,26 @@ def test_parser_container_bookkeeping():
     p.AddDecodingLayer("VXLAN")
     assert p.decoders == P.DEC_ETHERNET | P.DEC_IPV6 | P.DEC_VXLAN
     assert s.Decoder(L.LayerTypeVXLAN)[1]  # AddDecodingLayer Puts into the parser's container
+
+
+def test_endpoint_and_flow_constructors():
+    """flows.go:53-55,89-97,151-157,214-224 on the host: NewEndpoint / NewFlow bounds (a raw
+    longer than MaxEndpointSize panics in the reference), FlowFromEndpoints' type check and error
+    text, LessThan's order (type first, then the raw bytes lexicographically), Reverse, String."""
+    import pytest
+    from gopacket_amd.results import (EndpointIPv4, EndpointTCPPort, FlowFromEndpoints, MaxEndpointSize,
+                                      NewEndpoint, NewFlow)
+    assert MaxEndpointSize == 16
+    with pytest.raises(ValueError, match="greater than MaxEndpointSize"):
+        NewEndpoint(EndpointIPv4, bytes(17))
+    with pytest.raises(ValueError, match="greater than MaxEndpointSize"):
+        NewFlow(EndpointIPv4, bytes(4), bytes(17))
+    a, b = NewEndpoint(EndpointIPv4, bytes([10, 0, 0, 1])), NewEndpoint(EndpointIPv4, bytes([10, 0, 0, 2]))
+    f, err = FlowFromEndpoints(a, b)
+    assert err is None and f.Src() == a and f.Dst() == b and f.String() == "10.0.0.1->10.0.0.2"
+    assert f.Reverse().Src() == b and f.Reverse().Reverse() == f
+    _, err = FlowFromEndpoints(a, NewEndpoint(EndpointTCPPort, b"\x00\x50"))
+    assert str(err) == "Mismatched endpoint types: 1->4"
+    assert a.LessThan(b) and not b.LessThan(a) and not a.LessThan(a)
+    assert b.LessThan(NewEndpoint(EndpointTCPPort, b"\x00\x01"))  # type first
+    assert NewEndpoint(EndpointIPv4, b"\x0a").LessThan(a)  # a prefix sorts first (bytes.Compare)

@@ -637,6 +637,49 @@ def test_flows_from_results():
     assert seen >= {1, 4, 5}
 
 
+def test_fast_hash_of_built_flows_and_endpoints():
+    """gpd_fast_hash (ABI 9): Flow.FastHash / Endpoint.FastHash of caller-built keys on the device
+    (flows.go:60-83,167-174) against the oracle's FNV — raw lengths 0..16, EndpointTypes in and
+    beyond 32 bits (RegisterEndpointType numbers, negative int64), a flow and its Reverse(); and
+    NewFlow() copies of the mixed batch's decoded flows hash to what the decode kernel computed."""
+    from gopacket_amd import parser as P
+    from gopacket_amd.results import FastHashes, NewEndpoint, NewFlow
+    ol = O.lib()
+    M = (1 << 64) - 1
+
+    def ofnv(b):
+        return int(ol.gpo_fnv_hash(bytes(b), len(b)))
+
+    rng = np.random.default_rng(9)
+    typs = [1, 2, 4, 5, 1000, 77777, (1 << 40) + 3, -5, 0]
+    flows, eps, want_f, want_e = [], [], [], []
+    for k in range(600):
+        t = typs[k % len(typs)]
+        a = rng.integers(0, 256, int(rng.integers(0, 17)), dtype=np.uint8).tobytes()
+        b = rng.integers(0, 256, int(rng.integers(0, 17)), dtype=np.uint8).tobytes()
+        flows.append(NewFlow(t, a, b))
+        eps.append(NewEndpoint(t, a))
+        want_f.append((((ofnv(a) + ofnv(b)) & M) ^ (t & M)) * 1099511628211 & M)
+        want_e.append(((ofnv(a) ^ (t & M)) * 1099511628211) & M)
+        if 0 <= t < (1 << 32):
+            assert want_f[-1] == ol.gpo_flow_fasthash(t, a, len(a), b, len(b))
+            assert want_e[-1] == ol.gpo_endpoint_fasthash(t, a, len(a))
+    assert [int(x) for x in FastHashes(flows)] == want_f
+    assert [int(x) for x in FastHashes([f.Reverse() for f in flows])] == want_f
+    assert [int(x) for x in FastHashes(eps)] == want_e
+    assert flows[3].FastHash() == want_f[3] and eps[5].FastHash() == want_e[5]
+    mb = synth.make_mixed(2000)
+    p = P.NewDecodingLayerParser(L.LayerTypeEthernet, *[P.DECODER_BY_NAME[k]() for k in P.DECODER_BY_NAME])
+    dev = p.DecodeBatch(mb)
+    got, built = [], []
+    for i in range(mb.n):
+        for f in (dev.NetworkFlow(i, mb), dev.TransportFlow(i, mb)):
+            if f is not None:
+                got.append(f.FastHash())
+                built.append(NewFlow(f.EndpointType(), f.src, f.dst))
+    assert len(built) > 2000 and [int(x) for x in FastHashes(built)] == got
+
+
 def test_all_empty_batch():
     """A batch whose every packet is empty (CapLen 0, data_len 0): Ethernet's "too small" error
     for each, on the device and host paths."""
