@@ -931,6 +931,34 @@ def test_host_path_recovers_after_a_failed_call():
     assert_same(p.DecodeBatchHost(nxt), ref, nxt, ext=False)
 
 
+def test_host_path_chunks_with_everything_registered():
+    """The bench's PCIe-inclusive path over several chunks: batch, descriptors and result arrays
+    all registered, so every chunk's H2D and its results' D2H (on the slot's second stream) are
+    DMA straight from / into the caller's arrays while the next chunks travel — three 2^20-packet
+    chunks and a tail, against the device path."""
+    from gopacket_amd import parser as P
+    from gopacket_amd._lib import check, lib
+    from gopacket_amd.results import BatchResult
+    b = synth.make_udp64((3 << 20) + 4321)
+    p = P.DecodingLayerParser(L.LayerTypeEthernet)
+    p._mask = ALL
+    want = p.DecodeBatch(b, ext=False)
+    z = lambda dt: np.zeros(b.n, dt)
+    out = BatchResult(z(np.uint32), z(np.uint64), z(np.uint64), z(np.uint64), z(np.uint32), None,
+                      z(np.uint32))
+    arrs = [b.data, b.offset, b.caplen, out.status, out.layers, out.net_hash, out.tp_hash, out.csum,
+            out.hdr_off]
+    h = p.ctx().h
+    for a in arrs:
+        check(lib.gpd_host_register(h, a.ctypes.data, a.nbytes), "register")
+    try:
+        for _ in range(2):  # (the second call reuses the slots and their events)
+            assert_same(p.DecodeBatchHost(b, out=out), want, b, ext=False)
+    finally:
+        for a in arrs:
+            lib.gpd_host_unregister(h, a.ctypes.data)
+
+
 def test_host_paths_into_registered_result_arrays():
     """Result arrays registered with gpd_host_register receive the results by DMA (no staging
     copy): gpd_decode_host and gpd_decode_pcap_at must give the same words either way."""
