@@ -450,9 +450,9 @@ func (p *BatchDecodingLayerParser) FastHashes(flows []gopacket.Flow) ([]uint64, 
 		}
 	}
 	src := (*C.uint8_t)(bufs[1].p)
-	dst := (*C.uint8_t)(unsafe.Add(bufs[1].p, 16*n))
+	dst := (*C.uint8_t)(unsafe.Pointer(uintptr(bufs[1].p) + uintptr(16*n))) // (device memory: go 1.12's module)
 	if rc := C.gpd_fast_hash(C.int(p.device), C.uint64_t(n), (*C.int64_t)(bufs[0].p), src, (*C.uint8_t)(bufs[2].p),
-		dst, (*C.uint8_t)(unsafe.Add(bufs[2].p, n)), (*C.uint64_t)(bufs[3].p), nil); rc != C.GPD_OK {
+		dst, (*C.uint8_t)(unsafe.Pointer(uintptr(bufs[2].p) + uintptr(n))), (*C.uint64_t)(bufs[3].p), nil); rc != C.GPD_OK {
 		return nil, lastError("gpd_fast_hash", rc)
 	}
 	if e := C.hipMemcpy(unsafe.Pointer(&out[0]), bufs[3].p, C.size_t(8*n), C.hipMemcpyDeviceToHost); e != C.hipSuccess {
