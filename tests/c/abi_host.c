@@ -196,7 +196,7 @@ static int check_flows(gpd_ctx *ctx, hipStream_t s, const gpd_batch *db, const g
   /* record index -> export slot */
   uint64_t *pk = calloc(nrec + 1, 8), *by = calloc(nrec + 1, 8), *lo = calloc(nrec + 1, 8),
            *hi = calloc(nrec + 1, 8);
-  uint64_t assigned = 0, none = 0;
+  uint64_t assigned = 0, none = 0, *one = calloc(nrec + 1, 8);  /* a packet of each record */
   for (uint64_t i = 0; i < n && !bad; i++) {
     if (id[i] == GPD_FLOW_NONE) {
       none++;
@@ -210,6 +210,7 @@ static int check_flows(gpd_ctx *ctx, hipStream_t s, const gpd_batch *db, const g
       break;
     }
     const uint64_t seq = 1000 + i;
+    if (pk[k] == 0) one[k] = i;
     if (pk[k] == 0 || seq < lo[k]) lo[k] = seq;
     if (pk[k] == 0 || seq > hi[k]) hi[k] = seq;
     pk[k]++;
@@ -222,6 +223,44 @@ static int check_flows(gpd_ctx *ctx, hipStream_t s, const gpd_batch *db, const g
       fprintf(stderr, "flow: record %u counters differ\n", ridx[k]);
       bad = 1;
     }
+  /* gpd_fast_hash (ABI 9) of the records' network flows, rebuilt from their exported keys as
+   * NewFlow would hold them: each must equal the decode's NetworkFlow FastHash of its packets */
+  if (!bad && nrec > 0) {
+    int64_t *typ = calloc(nrec, 8);
+    uint8_t *raw = calloc(nrec, 32), *len = calloc(nrec, 2);
+    uint64_t *fh = calloc(nrec, 8), *nh = malloc(8 * n);
+    for (uint64_t k = 0; k < nrec; k++) {
+      typ[k] = rec[k].net_type;
+      memcpy(raw + 16 * k, rec[k].src, rec[k].addr_len);
+      memcpy(raw + 16 * (nrec + k), rec[k].dst, rec[k].addr_len);
+      len[k] = len[nrec + k] = rec[k].addr_len;
+    }
+    void *d_typ, *d_raw, *d_len, *d_fh;
+    HCHECK(hipMalloc(&d_typ, 8 * nrec));
+    HCHECK(hipMalloc(&d_raw, 32 * nrec));
+    HCHECK(hipMalloc(&d_len, 2 * nrec));
+    HCHECK(hipMalloc(&d_fh, 8 * nrec));
+    HCHECK(hipMemcpy(d_typ, typ, 8 * nrec, hipMemcpyHostToDevice));
+    HCHECK(hipMemcpy(d_raw, raw, 32 * nrec, hipMemcpyHostToDevice));
+    HCHECK(hipMemcpy(d_len, len, 2 * nrec, hipMemcpyHostToDevice));
+    int dev = 0;
+    HCHECK(hipGetDevice(&dev));
+    CHECK(gpd_fast_hash(dev, nrec, d_typ, d_raw, d_len, (uint8_t *)d_raw + 16 * nrec, (uint8_t *)d_len + nrec,
+                        d_fh, s));
+    HCHECK(hipStreamSynchronize(s));
+    HCHECK(hipMemcpy(fh, d_fh, 8 * nrec, hipMemcpyDeviceToHost));
+    HCHECK(hipMemcpy(nh, dr->net_hash, 8 * n, hipMemcpyDeviceToHost));
+    for (uint64_t k = 0; k < nrec && !bad; k++)
+      if (fh[k] != nh[one[k]]) {
+        fprintf(stderr, "flow: gpd_fast_hash of record %u differs from its packets' net hash\n", ridx[k]);
+        bad = 1;
+      }
+    HCHECK(hipFree(d_typ));
+    HCHECK(hipFree(d_raw));
+    HCHECK(hipFree(d_len));
+    HCHECK(hipFree(d_fh));
+    free(typ), free(raw), free(len), free(fh), free(nh);
+  }
   if (!bad) {
     qsort(rec, nrec, sizeof *rec, rec_key_cmp);
     for (uint64_t k = 1; k < nrec; k++)
@@ -239,7 +278,7 @@ static int check_flows(gpd_ctx *ctx, hipStream_t s, const gpd_batch *db, const g
   *flows_out = nrec;
   CHECK(gpd_flow_destroy(ft));
   HCHECK(hipFree(d_id));
-  free(id), free(rec), free(ridx), free(pk), free(by), free(lo), free(hi);
+  free(id), free(rec), free(ridx), free(pk), free(by), free(lo), free(hi), free(one);
   return bad;
 }
 
