@@ -1183,6 +1183,10 @@ def main():
     ap.add_argument("--lean", action="store_true", help="only the timed launches (profiling runs: "
                     "no 36-B record line, no fallback split, no CPU baseline)")
     args = ap.parse_args()
+    if "nodecode" in args.ablate or "nowait" in args.ablate:
+        # the stream-only ablations exist only in the diagnostic library (libgpd_diag.so,
+        # -DGPD_DIAG); the shipped libgpd.so refuses their option bits
+        os.environ["GPD_DIAGNOSTIC_LIBRARY"] = "1"
 
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and (args.gpus or 1) > 1:
@@ -1262,9 +1266,9 @@ def main():
     if "nohash" in args.ablate:
         parser.ComputeFlowHashes = False
     if "nodecode" in args.ablate:
-        parser._diag_options = 1 << 31  # kernel streams the windows and skips decoding
+        parser._diag_options = 1 << 31  # kernel streams the windows and skips decoding (diag lib)
     if "nowait" in args.ablate:
-        parser._diag_options = 1 << 30  # kernel skips the per-tile DMA wait (wrong results)
+        parser._diag_options = 1 << 30  # kernel skips the per-tile DMA wait (wrong results; diag lib)
     if "copy" in args.ablate:  # reference: device-to-device copy of the packet bytes
         src = dev_batch.data
         dst = torch.empty_like(src)

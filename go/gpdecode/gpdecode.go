@@ -153,16 +153,26 @@ var kindTypes = map[uint32][]gopacket.LayerType{
 // (parser.go:236-242): the decoders dlc holds replace the registered set, in place
 // (gpd_ctx_set_decoders; device and reloaded tables kept).  The engine registers decoder kinds
 // whole: a container holding a kind for only part of its CanDecode set (IPv6ExtensionSkipper for
-// some of 46..49) has no engine equivalent and is refused.
+// some of 46..49) has no engine equivalent and is refused, and so is a container holding, for a
+// layer type the engine decodes, a decoder it cannot run (decoderBit's error).  The parser keeps
+// its previous set on any error.
 func (p *BatchDecodingLayerParser) SetDecodingLayerContainer(dlc gopacket.DecodingLayerContainer) error {
 	var mask uint32
 	for bit, types := range kindTypes {
 		held := 0
 		for _, t := range types {
 			if d, ok := dlc.Decoder(t); ok {
-				if b, err := decoderBit(d); err == nil && b == bit {
-					held++
+				b, err := decoderBit(d)
+				if err != nil {
+					// a decoder the engine cannot run (a caller's own DecodingLayer for a
+					// type it takes): refused as NewBatchDecodingLayerParser refuses it, not
+					// dropped (its packets would stop with UnsupportedLayerType later)
+					return err
 				}
+				if b != bit {
+					return fmt.Errorf("gpdecode: the container holds %T for layer type %v, which the engine decodes with another kind", d, t)
+				}
+				held++
 			}
 		}
 		if held == len(types) {

@@ -9,7 +9,13 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
+# The product library.  bench.py's stream-only ablations (--ablate nodecode / nowait) set
+# GPD_DIAGNOSTIC_LIBRARY=1 to load libgpd_diag.so instead: the same sources built with
+# -DGPD_DIAG, whose runtime accepts the two ablation option bits that libgpd.so refuses.
 LIB_PATH = os.path.join(_HERE, "libgpd.so")
+DIAG_LIB_PATH = os.path.join(_HERE, "libgpd_diag.so")
+if os.environ.get("GPD_DIAGNOSTIC_LIBRARY") == "1":
+    LIB_PATH = DIAG_LIB_PATH
 
 GPD_ABI_VERSION = 9
 GPD_OK = 0
@@ -145,7 +151,7 @@ def _load():
         fn.restype = res
         fn.argtypes = args
     if lib.gpd_abi_version() != GPD_ABI_VERSION:
-        raise ImportError("gopacket_amd: libgpd.so ABI version mismatch")
+        raise ImportError(f"gopacket_amd: {os.path.basename(LIB_PATH)} ABI version mismatch")
     return lib
 
 

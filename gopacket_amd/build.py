@@ -1,6 +1,7 @@
 """Build the in-tree native libraries.
 
   gopacket_amd/libgpd.so       product: HIP kernels (gfx950) + C-ABI runtime (include/gpd.h)
+  gopacket_amd/libgpd_diag.so  diagnostics only (--diag): the same with -DGPD_DIAG (bench --ablate)
   oracle/libgpd_oracle.so      test infrastructure: CPU restatement (oracle/)
   tests/c/abi_host             test driver: a plain C host on the C-ABI (no Python/torch)
   gopacket_amd/libgpd_synth.so workload generator for the bench (config 5 captures); not product
@@ -14,6 +15,7 @@ from __future__ import annotations
 import os
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "gopacket_amd")
@@ -22,6 +24,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("GPD_OFFLOAD_ARCH", "gfx950")
 
 LIB = os.path.join(PKG, "libgpd.so")
+DIAG_LIB = os.path.join(PKG, "libgpd_diag.so")
 ORACLE_LIB = os.path.join(ROOT, "oracle", "libgpd_oracle.so")
 
 SOURCES = [os.path.join(CSRC, "gpd_kernels.hip"), os.path.join(CSRC, "gpd_runtime.cpp"),
@@ -40,17 +43,32 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_lib(force: bool = False, verbose: bool = False) -> str:
-    if force or _stale(LIB, SOURCES + HEADERS):
-        extra = os.environ.get("GPD_EXTRA_CFLAGS", "").split()  # diagnostic builds (tools/)
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-               "-Wall", "-Wno-unused-function", "-pthread", "-I", os.path.join(ROOT, "include"),
-               *extra, *SOURCES, "-o", LIB + ".tmp"]
+def build_lib(force: bool = False, verbose: bool = False, diag: bool = False) -> str:
+    """libgpd.so, or with diag=True libgpd_diag.so: the same sources with -DGPD_DIAG, whose
+    runtime also takes bench.py's stream-only ablation bits (never loaded by the product)."""
+    out = DIAG_LIB if diag else LIB
+    if force or _stale(out, SOURCES + HEADERS):
+        extra = os.environ.get("GPD_EXTRA_CFLAGS", "").split()  # A/B builds (tools/)
+        if diag:
+            extra.append("-DGPD_DIAG")
+        # one hipcc per source in parallel (the kernels' TU dominates), then one link
+        objdir = os.path.join(ROOT, "build", "diag" if diag else "lib")
+        os.makedirs(objdir, exist_ok=True)
+        base = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
+                "-Wno-unused-function", "-pthread", "-I", os.path.join(ROOT, "include"), *extra]
+        objs = [os.path.join(objdir, os.path.basename(src) + ".o") for src in SOURCES]
+        cmds = [base + ["-c", src, "-o", obj] for src, obj in zip(SOURCES, objs)]
         if verbose:
-            print(" ".join(cmd), flush=True)
-        subprocess.run(cmd, check=True)
-        os.replace(LIB + ".tmp", LIB)
-    return LIB
+            for c in cmds:
+                print(" ".join(c), flush=True)
+        with ThreadPoolExecutor(max_workers=min(len(cmds), os.cpu_count() or 1)) as ex:
+            for r in list(ex.map(lambda c: subprocess.run(c), cmds)):
+                if r.returncode != 0:
+                    raise subprocess.CalledProcessError(r.returncode, r.args)
+        subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", *objs,
+                        "-o", out + ".tmp"], check=True)
+        os.replace(out + ".tmp", out)
+    return out
 
 
 def build_oracle(force: bool = False) -> str:
@@ -106,6 +124,8 @@ def build_abi_host(force: bool = False) -> str:
 if __name__ == "__main__":
     force = "--force" in sys.argv
     print(build_lib(force=force, verbose=True))
+    if "--diag" in sys.argv:
+        print(build_lib(force=force, verbose=True, diag=True))
     print(build_oracle(force=force))
     print(build_abi_host(force=force))
     print(build_synth(force=force))

@@ -301,7 +301,8 @@ int gpd_decode_tpv3(gpd_ctx *ctx, const gpd_tpv3_ring *ring, uint32_t first_bloc
   if (data_len > 0xFFFFFFF0ull)
     return gpd::set_error(GPD_ERR_INVALID, "gpd_decode_tpv3: %llu walked bytes exceed one batch",
                           (unsigned long long)data_len);
-  if (hipSetDevice(gpd::ctx_device(ctx)) != hipSuccess)
+  gpd::DeviceScope dscope_;
+  if (dscope_.set(gpd::ctx_device(ctx)) != hipSuccess)
     return gpd::set_error(GPD_ERR_HIP, "gpd_decode_tpv3: hipSetDevice");
   // context scratch slots 0-8 (kept across calls: a ring is walked again and again)
   auto *d_data = static_cast<uint8_t *>(gpd::ctx_scratch(ctx, 0, ((data_len + 15) & ~15ull) + 64));

@@ -653,7 +653,8 @@ int gpd_fast_hash(int device, uint64_t n, const int64_t *typ, const uint8_t *src
     return gpd::set_error(GPD_ERR_INVALID, "gpd_fast_hash: null argument");
   if (((uintptr_t)src | (uintptr_t)(dst ? dst : src)) & 15u)
     return gpd::set_error(GPD_ERR_INVALID, "gpd_fast_hash: raw arrays must be 16-byte aligned");
-  FLOW_TRY(hipSetDevice(device));
+  gpd::DeviceScope dscope_;
+  FLOW_TRY(dscope_.set(device));
   int cus = 0;
   FLOW_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
   const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, (uint64_t)std::max(cus, 1) * 8);
@@ -676,7 +677,8 @@ int gpd_flow_create(gpd_ctx *ctx, uint64_t capacity, gpd_flowtable **out) {
   ft->device = gpd::ctx_device(ctx);
   ft->num_cus = gpd::ctx_num_cus(ctx);
   ft->cap = cap;
-  hipError_t e = hipSetDevice(ft->device);
+  gpd::DeviceScope dscope_;
+  hipError_t e = dscope_.set(ft->device);
   if (e == hipSuccess) e = hipMalloc(&ft->tab, cap * sizeof(gpd::FlowHot));
   if (e == hipSuccess) e = hipMalloc(&ft->cold, cap * sizeof(gpd::FlowCold));
   if (e == hipSuccess) e = hipMalloc(&ft->stats, gpd::stat_at(gpd::FS_WORDS) * sizeof(unsigned long long));
@@ -697,7 +699,8 @@ int gpd_flow_create(gpd_ctx *ctx, uint64_t capacity, gpd_flowtable **out) {
 
 int gpd_flow_reset(gpd_flowtable *ft, void *stream) {
   if (!ft) return gpd::set_error(GPD_ERR_INVALID, "gpd_flow_reset: null table");
-  FLOW_TRY(hipSetDevice(ft->device));
+  gpd::DeviceScope dscope_;
+  FLOW_TRY(dscope_.set(ft->device));
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(gpd::flow_reset_kernel, dim3(grid_for(ft->cap, ft->num_cus)),
                      dim3(gpd::kFlowThreads), 0, s, ft->tab, ft->cold, ft->cap);
@@ -717,7 +720,8 @@ int gpd_flow_insert(gpd_flowtable *ft, const gpd_batch *in, const gpd_result *re
   if (in->n == 0) return GPD_OK;
   if (!in->data || !in->offset || !in->caplen)
     return gpd::set_error(GPD_ERR_INVALID, "gpd_flow_insert: null batch array");
-  FLOW_TRY(hipSetDevice(ft->device));
+  gpd::DeviceScope dscope_;
+  FLOW_TRY(dscope_.set(ft->device));
   gpd::FlowParams P{in->data, in->data_len, in->offset, in->caplen, res->status, res->hdr_off,
                     flow_id, in->n, index_base, ft->tab, ft->cap - 1, ft->stats,
                     nullptr, nullptr, nullptr, nullptr, nullptr, 0};
@@ -754,7 +758,8 @@ int gpd_flow_keys(gpd_flowtable *ft, const gpd_batch *in, const gpd_result *res,
   if (in->n == 0) return GPD_OK;
   if (!in->data || !in->offset || !in->caplen)
     return gpd::set_error(GPD_ERR_INVALID, "gpd_flow_keys: null batch array");
-  FLOW_TRY(hipSetDevice(ft->device));
+  gpd::DeviceScope dscope_;
+  FLOW_TRY(dscope_.set(ft->device));
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid(grid_for(in->n, ft->num_cus)), block(gpd::kFlowThreads);
   const uint64_t L = (uint64_t)nparts * grid.x, words = L + 1 + nparts;
@@ -789,7 +794,8 @@ int gpd_flow_key_ids(gpd_flowtable *ft, const gpd_flow_key *keys, uint64_t m, co
   if (!ft || (m && (!keys || !ids)) || (n && (!owner || !flow_id)))
     return gpd::set_error(GPD_ERR_INVALID, "gpd_flow_key_ids: null argument");
   if (n == 0) return GPD_OK;
-  FLOW_TRY(hipSetDevice(ft->device));
+  gpd::DeviceScope dscope_;
+  FLOW_TRY(dscope_.set(ft->device));
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(gpd::flow_ids_fill_kernel, dim3(grid_for(n, ft->num_cus)), dim3(gpd::kFlowThreads),
                      0, s, owner, flow_id, n);
@@ -807,7 +813,8 @@ int gpd_flow_insert_keys(gpd_flowtable *ft, const gpd_flow_key *keys, uint64_t n
   if (!ft || (n && (!keys || !flow_id)))
     return gpd::set_error(GPD_ERR_INVALID, "gpd_flow_insert_keys: null argument");
   if (n == 0) return GPD_OK;
-  FLOW_TRY(hipSetDevice(ft->device));
+  gpd::DeviceScope dscope_;
+  FLOW_TRY(dscope_.set(ft->device));
   gpd::FlowParams P{nullptr, 0, nullptr, nullptr, nullptr, nullptr, flow_id, n, 0, ft->tab,
                     ft->cap - 1, ft->stats, keys, nullptr, nullptr, nullptr, nullptr, 0};
   FLOW_TRY(grow_made(ft, n));
@@ -828,7 +835,8 @@ int gpd_flow_insert_keys(gpd_flowtable *ft, const gpd_flow_key *keys, uint64_t n
 
 int gpd_flow_stats_get(gpd_flowtable *ft, gpd_flow_stats *out, void *stream) {
   if (!ft || !out) return gpd::set_error(GPD_ERR_INVALID, "gpd_flow_stats_get: null argument");
-  FLOW_TRY(hipSetDevice(ft->device));
+  gpd::DeviceScope dscope_;
+  FLOW_TRY(dscope_.set(ft->device));
   unsigned long long hs[gpd::stat_at(gpd::FS_WORDS)], h[gpd::FS_WORDS];
   FLOW_TRY(hipMemcpyAsync(hs, ft->stats, sizeof hs, hipMemcpyDeviceToHost, (hipStream_t)stream));
   FLOW_TRY(hipStreamSynchronize((hipStream_t)stream));
@@ -846,7 +854,8 @@ int gpd_flow_export(gpd_flowtable *ft, gpd_flow_rec *out, uint32_t *rec_index, u
                     uint64_t *n, void *stream) {
   if (!ft || !out || !n) return gpd::set_error(GPD_ERR_INVALID, "gpd_flow_export: null argument");
   *n = 0;
-  FLOW_TRY(hipSetDevice(ft->device));
+  gpd::DeviceScope dscope_;
+  FLOW_TRY(dscope_.set(ft->device));
   hipStream_t s = (hipStream_t)stream;
   gpd_flow_stats st;
   int rc = gpd_flow_stats_get(ft, &st, stream);
@@ -901,7 +910,8 @@ int gpd_flow_test_counter_bits(gpd_flowtable *ft, uint32_t bits) {
 
 int gpd_flow_destroy(gpd_flowtable *ft) {
   if (!ft) return GPD_OK;
-  (void)hipSetDevice(ft->device);
+  gpd::DeviceScope dscope_;
+  (void)dscope_.set(ft->device);
   if (ft->tab) (void)hipFree(ft->tab);
   if (ft->cold) (void)hipFree(ft->cold);
   if (ft->stats) (void)hipFree(ft->stats);

@@ -7,6 +7,23 @@
 
 namespace gpd {
 
+// Every C-ABI entry point that selects its context's device restores the caller's current
+// device on return: a Go thread or a torch process calling in with another device
+// current keeps it.  `set` switches only when needed; the destructor switches back.
+struct DeviceScope {
+  int prev = -1;
+  DeviceScope() {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+  }
+  hipError_t set(int device) { return device == prev ? hipSuccess : hipSetDevice(device); }
+  ~DeviceScope() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+  DeviceScope(const DeviceScope &) = delete;
+  DeviceScope &operator=(const DeviceScope &) = delete;
+};
+
 // ---- device dispatch tables ---------------------------------------------------------
 // Two encodings of the same four reference tables (ethertype[65536], ipproto[256],
 // tcp_port[65536], udp_port[65536]; layers/enums.go:304-345, layers/ports.go:62-122):

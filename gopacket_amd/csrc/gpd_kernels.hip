@@ -41,15 +41,25 @@
 namespace gpd {
 
 constexpr uint64_t kGridRounds = 4;  // a launch covers at most 4 rounds of resident workgroups
-constexpr uint32_t kDiagSkipDecode = 1u << 31;  // internal diagnostic option (bench --ablate nodecode)
-constexpr uint32_t kDiagNoWait = 1u << 30;      // internal diagnostic: skip the per-tile DMA wait
+// The two diagnostic bits (bench --ablate nodecode / nowait) exist only in the diagnostic
+// library (libgpd_diag.so, built with -DGPD_DIAG): there the runtime accepts them; in the
+// shipped libgpd.so they are refused by gpd_ctx_set_options / gpd_ctx_create and every branch
+// that reads them compiles away (kDiagBuild false => both constants 0).
+#ifdef GPD_DIAG
+constexpr bool kDiagBuild = true;
+#else
+constexpr bool kDiagBuild = false;
+#endif
+constexpr uint32_t kDiagSkipDecodeBit = 1u << 31, kDiagNoWaitBit = 1u << 30;
+constexpr uint32_t kDiagSkipDecode = kDiagBuild ? kDiagSkipDecodeBit : 0u;  // stream only, no decode
+constexpr uint32_t kDiagNoWait = kDiagBuild ? kDiagNoWaitBit : 0u;          // skip the per-tile DMA wait
 constexpr uint32_t kDiagNtLoad = 1u << 29;      // A/B: window LDS-DMA with the nt cache policy
 constexpr uint32_t kDiagNtStore = 1u << 28;     // A/B: result stores with the nt cache policy
 constexpr uint32_t kShiftWindows = 1u << 27;    // internal: register-staged windows copied shifted
 constexpr uint32_t kRegPrefix = 1u << 26;       // internal: 8 KiB windows of long frames (IMIX)
 constexpr uint32_t kHeaderOnce = 1u << 25;      // internal: 8 KiB windows decoded once per tile (seg_pass)
 constexpr uint32_t kRounds = 1u << 24;          // internal: header-once over 8 KiB rounds (ro_kernel)
-constexpr uint32_t kDiagMask = kDiagSkipDecode | kDiagNoWait | kDiagNtLoad | kDiagNtStore | kShiftWindows |
+constexpr uint32_t kDiagMask = kDiagSkipDecodeBit | kDiagNoWaitBit | kDiagNtLoad | kDiagNtStore | kShiftWindows |
                                kRegPrefix | kHeaderOnce | kRounds;
 // A/B builds only (GPD_EXTRA_CFLAGS=-DGPD_EXP=..., tools/ab_exp.sh): a fast-path variant under
 // test reads kExp inside an `#if GPD_EXP` block; the shipped library has none.
@@ -1896,7 +1906,7 @@ __device__ __forceinline__ void rows_prefix(const uint32_t (&cs)[NC], uint32_t p
 // is issued and the wait at the next commit covers exactly those loads)  ->  plan and load
 // window k+1  ->  decode window k from LDS.
 template <int STAGE, bool CS, bool HASH, int MINW, bool DEFER = false, bool RPFX = true, bool HO = false,
-          bool AL = false, bool DIAG = true>
+          bool AL = false, bool DIAG = kDiagBuild>
 __global__ __launch_bounds__(256, MINW) void rs_kernel(KParams P) {
   constexpr int WAVES = 4;
   constexpr int NC = STAGE / 1024;              // 16-byte chunks per lane per window
@@ -2472,7 +2482,7 @@ static hipError_t launch_t(const KParams &P, hipStream_t stream, int num_cus) {
 }
 
 template <int STAGE, bool CS, bool HASH, int MINW, bool DEFER = false, bool RPFX = true, bool HO = false,
-          bool AL = false, bool DIAG = true>
+          bool AL = false, bool DIAG = false>
 static hipError_t launch_rs(KParams &P, hipStream_t stream, int num_cus) {
   const uint64_t ntiles = (P.n + 63) / 64;
   const size_t lds = ((P.image_words * 4u + 15u) & ~15u) + 4 * (size_t)rs_wave_lds_bytes(STAGE) + 64;
@@ -2516,6 +2526,20 @@ static hipError_t launch_fast(KParams &P, hipStream_t stream, int num_cus) {
     if (P.waves == 2) return launch_ro<CS, HASH, 2>(P, stream, num_cus);
     return launch_ro<CS, HASH, 3>(P, stream, num_cus);
   }
+  if constexpr (kDiagBuild) {  // libgpd_diag.so: the skeleton (no decode) instantiations
+    if (P.options & kDiagSkipDecode) {
+      if (P.stage == 4096) {
+        if (P.waves == 2) return launch_rs<4096, CS, HASH, 2, false, true, false, false, true>(P, stream, num_cus);
+        if (P.waves == 3) return launch_rs<4096, CS, HASH, 3, false, true, false, false, true>(P, stream, num_cus);
+        return launch_rs<4096, CS, HASH, 4, false, true, false, false, true>(P, stream, num_cus);
+      }
+      if (P.options & kHeaderOnce) return launch_rs<8192, CS, HASH, 3, false, true, true, false, true>(P, stream, num_cus);
+      if (P.options & kRegPrefix) return launch_rs<8192, CS, HASH, 3, false, true, false, false, true>(P, stream, num_cus);
+      if (!(P.options & kShiftWindows))
+        return launch_rs<8192, CS, HASH, 3, false, false, false, true, true>(P, stream, num_cus);
+      return launch_rs<8192, CS, HASH, 3, false, false, false, false, true>(P, stream, num_cus);
+    }
+  }
   if (P.stage == 4096) {
     if (P.waves == 2) return launch_rs<4096, CS, HASH, 2>(P, stream, num_cus);
     if (P.waves == 3) return launch_rs<4096, CS, HASH, 3>(P, stream, num_cus);
@@ -2530,14 +2554,10 @@ static hipError_t launch_fast(KParams &P, hipStream_t stream, int num_cus) {
   // unshifted windows of mid-sized frames (VXLAN's 128 B): the aligned-chunk transport checksum
   // and the inner Ethernet bytes from registers (fast_decode AL); shifted windows (pcap records,
   // 65..96-B slots) keep the plain kernel, where both cost ~1 % (measured A/B)
-  // (these two are compiled without the skeleton diagnostic unless it is asked for: config 4
-  // -2.2 %, pcap64 -0.7 %, the loop schedules better; measured A/B on one box)
-  const bool diag = (P.options & kDiagSkipDecode) != 0;
-  if (!(P.options & kShiftWindows))
-    return diag ? launch_rs<8192, CS, HASH, 3, false, false, false, true, true>(P, stream, num_cus)
-                : launch_rs<8192, CS, HASH, 3, false, false, false, true, false>(P, stream, num_cus);
-  return diag ? launch_rs<8192, CS, HASH, 3, false, false, false, false, true>(P, stream, num_cus)
-              : launch_rs<8192, CS, HASH, 3, false, false, false, false, false>(P, stream, num_cus);
+  // (every shipped kernel is compiled without the skeleton diagnostic's branch: round 4
+  // measured config 4 -2.2 %, pcap64 -0.7 %; round 6 the 4 KiB kernels too)
+  if (!(P.options & kShiftWindows)) return launch_rs<8192, CS, HASH, 3, false, false, false, true>(P, stream, num_cus);
+  return launch_rs<8192, CS, HASH, 3, false, false>(P, stream, num_cus);
 }
 
 // The generic decoder over LDS windows (ext records, other first layers, PAGES tables): the

@@ -323,13 +323,17 @@ void gpd_default_tables(uint16_t *ethertype, uint16_t *ipproto, uint16_t *tcp_po
 
 // The LDS image (and the PAGES blob when the tables do not hash) from ctx's decoder mask and
 // its table snapshot.
-static int build_image(gpd_ctx *ctx) {
-  const std::vector<uint16_t> &eth = ctx->t_eth, &proto = ctx->t_proto, &tcp = ctx->t_tcp,
-                              &udp = ctx->t_udp;
+// Builds the dispatch image (and the PAGES blob) of `decoders` over the given tables into new
+// device buffers; only when every step succeeded are they swapped into ctx (the old ones
+// freed), so a failed rebuild leaves the context exactly as it was.  The callers
+// commit their decoder mask / table snapshot after a GPD_OK only.
+static int build_image(gpd_ctx *ctx, uint32_t decoders, const std::vector<uint16_t> &eth,
+                       const std::vector<uint16_t> &proto, const std::vector<uint16_t> &tcp,
+                       const std::vector<uint16_t> &udp) {
   // LDS image: LUT (32 words) + ipproto with LUT entries (256 words) + the three hashes
   std::vector<uint32_t> img(gpd::kHashLutWords + gpd::kHashProtoWords, 0);
   uint8_t *lut = reinterpret_cast<uint8_t *>(img.data());
-  type_lut(ctx->decoders, lut);
+  type_lut(decoders, lut);
   for (uint32_t p = 0; p < 256; p++) {
     const uint32_t lt = proto[p];
     img[gpd::kHashLutWords + p] = lt | ((lt < 128 ? lut[lt] : 0xFFu) << 16);
@@ -337,9 +341,9 @@ static int build_image(gpd_ctx *ctx) {
   std::vector<uint32_t> he, ht, hu;
   const uint32_t room = gpd::kHashMaxWords - (uint32_t)img.size();
   uint32_t me = 0, mt = 0, mu = 0, be = 0, bt = 0, bu = 0;
-  ctx->fixed = build_fixed(eth.data(), tcp.data(), udp.data(), lut, he, ht, hu, me);
-  bool hashed = ctx->fixed;
-  if (ctx->fixed) {
+  const bool fixed = build_fixed(eth.data(), tcp.data(), udp.data(), lut, he, ht, hu, me);
+  bool hashed = fixed;
+  if (fixed) {
     mt = mu = me;
     be = bt = bu = gpd::kFixBits;
   } else {
@@ -347,53 +351,80 @@ static int build_image(gpd_ctx *ctx) {
              build_hash(tcp.data(), lut, room / 4, ht, mt, bt) &&
              build_hash(udp.data(), lut, room / 4, hu, mu, bu);
   }
-  HIP_TRY(hipSetDevice(ctx->device));
-  if (ctx->d_image) { HIP_TRY(hipFree(ctx->d_image)); ctx->d_image = nullptr; }
-  if (ctx->d_pages) { HIP_TRY(hipFree(ctx->d_pages)); ctx->d_pages = nullptr; }
+  uint32_t eth_base = 0, tcp_base = 0, udp_base = 0;
+  std::vector<uint16_t> blob;
   if (hashed) {  // every hash starts on an 8-byte boundary (ds_read_b64 buckets)
-    ctx->use_pages = 0;
     auto put = [&](const std::vector<uint32_t> &h, uint32_t &base) {
       if (img.size() & 1) img.push_back(0);
       base = (uint32_t)img.size();
       img.insert(img.end(), h.begin(), h.end());
     };
-    put(he, ctx->eth_base); ctx->eth_bits = be; ctx->eth_mult = me;
-    put(ht, ctx->tcp_base); ctx->tcp_bits = bt; ctx->tcp_mult = mt;
-    put(hu, ctx->udp_base); ctx->udp_bits = bu; ctx->udp_mult = mu;
-    if (ctx->fixed && (ctx->eth_base != gpd::kFixEthBase || ctx->tcp_base != gpd::kFixTcpBase ||
-                       ctx->udp_base != gpd::kFixUdpBase))
+    put(he, eth_base);
+    put(ht, tcp_base);
+    put(hu, udp_base);
+    if (fixed && (eth_base != gpd::kFixEthBase || tcp_base != gpd::kFixTcpBase || udp_base != gpd::kFixUdpBase))
       return set_err(GPD_ERR_INVALID, "internal: fixed table layout mismatch");
   } else {
-    ctx->use_pages = 1;
-    std::vector<uint16_t> blob = encode_tables(eth.data(), proto.data(), tcp.data(), udp.data());
-    HIP_TRY(hipMalloc(&ctx->d_pages, blob.size() * sizeof(uint16_t)));
-    HIP_TRY(hipMemcpy(ctx->d_pages, blob.data(), blob.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+    blob = encode_tables(eth.data(), proto.data(), tcp.data(), udp.data());
   }
+  gpd::DeviceScope dscope_;
+  HIP_TRY(dscope_.set(ctx->device));
+  uint32_t *d_image = nullptr;
+  uint16_t *d_pages = nullptr;
+  hipError_t e = hipMalloc(&d_image, img.size() * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMemcpy(d_image, img.data(), img.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+  if (e == hipSuccess && !hashed) e = hipMalloc(&d_pages, blob.size() * sizeof(uint16_t));
+  if (e == hipSuccess && !hashed)
+    e = hipMemcpy(d_pages, blob.data(), blob.size() * sizeof(uint16_t), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    if (d_image) (void)hipFree(d_image);
+    if (d_pages) (void)hipFree(d_pages);
+    return set_err(e == hipErrorOutOfMemory ? GPD_ERR_NOMEM : GPD_ERR_HIP, "dispatch image: %s",
+                   hipGetErrorString(e));
+  }
+  if (ctx->d_image) (void)hipFree(ctx->d_image);
+  if (ctx->d_pages) (void)hipFree(ctx->d_pages);
+  ctx->d_image = d_image;
+  ctx->d_pages = d_pages;
   ctx->image_words = (uint32_t)img.size();
-  HIP_TRY(hipMalloc(&ctx->d_image, img.size() * sizeof(uint32_t)));
-  HIP_TRY(hipMemcpy(ctx->d_image, img.data(), img.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  ctx->fixed = fixed;
+  ctx->use_pages = hashed ? 0 : 1;
+  if (hashed) {
+    ctx->eth_base = eth_base; ctx->eth_bits = be; ctx->eth_mult = me;
+    ctx->tcp_base = tcp_base; ctx->tcp_bits = bt; ctx->tcp_mult = mt;
+    ctx->udp_base = udp_base; ctx->udp_bits = bu; ctx->udp_mult = mu;
+  }
   return GPD_OK;
 }
 
 int gpd_ctx_reload_tables(gpd_ctx *ctx, const gpd_config *cfg) {
   if (!ctx || !cfg) return set_err(GPD_ERR_INVALID, "gpd_ctx_reload_tables: null argument");
-  ctx->t_eth.assign(65536, 0);
-  ctx->t_proto.assign(256, 0);
-  ctx->t_tcp.assign(65536, 0);
-  ctx->t_udp.assign(65536, 0);
-  gpd_default_tables(ctx->t_eth.data(), ctx->t_proto.data(), ctx->t_tcp.data(), ctx->t_udp.data());
-  if (cfg->ethertype) std::memcpy(ctx->t_eth.data(), cfg->ethertype, 65536 * 2);
-  if (cfg->ipproto) std::memcpy(ctx->t_proto.data(), cfg->ipproto, 256 * 2);
-  if (cfg->tcp_port) std::memcpy(ctx->t_tcp.data(), cfg->tcp_port, 65536 * 2);
-  if (cfg->udp_port) std::memcpy(ctx->t_udp.data(), cfg->udp_port, 65536 * 2);
-  return build_image(ctx);
+  std::vector<uint16_t> eth(65536, 0), proto(256, 0), tcp(65536, 0), udp(65536, 0);
+  gpd_default_tables(eth.data(), proto.data(), tcp.data(), udp.data());
+  if (cfg->ethertype) std::memcpy(eth.data(), cfg->ethertype, 65536 * 2);
+  if (cfg->ipproto) std::memcpy(proto.data(), cfg->ipproto, 256 * 2);
+  if (cfg->tcp_port) std::memcpy(tcp.data(), cfg->tcp_port, 65536 * 2);
+  if (cfg->udp_port) std::memcpy(udp.data(), cfg->udp_port, 65536 * 2);
+  const int rc = build_image(ctx, ctx->decoders, eth, proto, tcp, udp);
+  if (rc != GPD_OK) return rc;  // the context keeps its previous snapshot and image
+  ctx->t_eth.swap(eth);
+  ctx->t_proto.swap(proto);
+  ctx->t_tcp.swap(tcp);
+  ctx->t_udp.swap(udp);
+  return GPD_OK;
 }
 
-// Options the caller may set: the reference's two fields, the engine knobs and the two
-// diagnostic bits bench.py uses (bits 24-29 are the runtime's own launch flags).
+// Options the caller may set: the reference's two fields and the engine knobs (bits 24-29
+// are the runtime's own launch flags).  The diagnostic library (libgpd_diag.so, -DGPD_DIAG)
+// also takes bench.py's two ablation bits (30: no DMA wait, 31: no decode), which give wrong
+// results by design; the shipped libgpd.so refuses them like any unknown bit (gpd.h).
+#ifdef GPD_DIAG
+static constexpr uint32_t kDiagOptions = (1u << 30) | (1u << 31);
+#else
+static constexpr uint32_t kDiagOptions = 0;
+#endif
 static constexpr uint32_t kUserOptions = GPD_OPT_IGNORE_UNSUPPORTED | GPD_OPT_IGNORE_PANIC |
-                                         GPD_OPT_NO_CHECKSUMS | GPD_OPT_NO_FLOW_HASH |
-                                         (1u << 30) | (1u << 31);
+                                         GPD_OPT_NO_CHECKSUMS | GPD_OPT_NO_FLOW_HASH | kDiagOptions;
 
 int gpd_ctx_set_options(gpd_ctx *ctx, uint32_t options) {
   if (!ctx) return set_err(GPD_ERR_INVALID, "gpd_ctx_set_options: ctx is NULL");
@@ -409,8 +440,9 @@ int gpd_ctx_set_decoders(gpd_ctx *ctx, uint32_t decoders) {
   if (decoders & ~GPD_DEC_ALL)
     return set_err(GPD_ERR_INVALID, "gpd_ctx_set_decoders: unknown decoder bits 0x%x", decoders);
   if (decoders == ctx->decoders) return GPD_OK;
-  ctx->decoders = decoders;
-  return build_image(ctx);
+  const int rc = build_image(ctx, decoders, ctx->t_eth, ctx->t_proto, ctx->t_tcp, ctx->t_udp);
+  if (rc == GPD_OK) ctx->decoders = decoders;  // a failed rebuild keeps the old mask and image
+  return rc;
 }
 
 int gpd_ctx_add_decoders(gpd_ctx *ctx, uint32_t decoders) {
@@ -418,8 +450,10 @@ int gpd_ctx_add_decoders(gpd_ctx *ctx, uint32_t decoders) {
   if (decoders & ~GPD_DEC_ALL)
     return set_err(GPD_ERR_INVALID, "gpd_ctx_add_decoders: unknown decoder bits 0x%x", decoders);
   if ((ctx->decoders | decoders) == ctx->decoders) return GPD_OK;
-  ctx->decoders |= decoders;
-  return build_image(ctx);
+  const uint32_t next = ctx->decoders | decoders;
+  const int rc = build_image(ctx, next, ctx->t_eth, ctx->t_proto, ctx->t_tcp, ctx->t_udp);
+  if (rc == GPD_OK) ctx->decoders = next;
+  return rc;
 }
 
 int gpd_ctx_create(int device, const gpd_config *cfg, gpd_ctx **out) {
@@ -449,7 +483,8 @@ int gpd_ctx_create(int device, const gpd_config *cfg, gpd_ctx **out) {
   }
   ctx->options = cfg->options;
   hipDeviceProp_t prop;
-  if (hipSetDevice(device) != hipSuccess || hipGetDeviceProperties(&prop, device) != hipSuccess) {
+  gpd::DeviceScope dscope_;
+  if (dscope_.set(device) != hipSuccess || hipGetDeviceProperties(&prop, device) != hipSuccess) {
     delete ctx;
     return set_err(GPD_ERR_HIP, "gpd_ctx_create: cannot query device %d", device);
   }
@@ -501,7 +536,8 @@ static void free_slots(gpd_ctx *ctx) {
 
 int gpd_ctx_destroy(gpd_ctx *ctx) {
   if (!ctx) return GPD_OK;
-  (void)hipSetDevice(ctx->device);
+  gpd::DeviceScope dscope_;
+  (void)dscope_.set(ctx->device);
   free_slots(ctx);
   if (ctx->d_image) (void)hipFree(ctx->d_image);
   if (ctx->d_pages) (void)hipFree(ctx->d_pages);
@@ -525,7 +561,8 @@ int gpd_last_launch_split(gpd_ctx *ctx, uint64_t *fallback, float *fast_ms, floa
   if (!ctx->timed || !ctx->timed_split)
     return set_err(GPD_ERR_INVALID, "gpd_last_launch_split: no timed fast-path launch "
                                     "(gpd_ctx_set_timing(1), then one gpd_decode of <= 2^30 packets)");
-  HIP_TRY(hipSetDevice(ctx->device));
+  gpd::DeviceScope dscope_;
+  HIP_TRY(dscope_.set(ctx->device));
   HIP_TRY(hipEventSynchronize(ctx->ev1));
   HIP_TRY(hipEventElapsedTime(fast_ms, ctx->ev0, ctx->evm));
   HIP_TRY(hipEventElapsedTime(list_ms, ctx->evm, ctx->ev1));
@@ -558,7 +595,8 @@ int gpd_ctx_set_tuning(gpd_ctx *ctx, const gpd_tuning *t) {
 
 int gpd_ctx_set_timing(gpd_ctx *ctx, int enable) {
   if (!ctx) return set_err(GPD_ERR_INVALID, "gpd_ctx_set_timing: null ctx");
-  HIP_TRY(hipSetDevice(ctx->device));
+  gpd::DeviceScope dscope_;
+  HIP_TRY(dscope_.set(ctx->device));
   if (enable && !ctx->ev0) {
     HIP_TRY(hipEventCreate(&ctx->ev0));
     HIP_TRY(hipEventCreate(&ctx->ev1));
@@ -724,13 +762,15 @@ int gpd_decode(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, void *s
   if (!ctx) return set_err(GPD_ERR_INVALID, "gpd_decode: null ctx");
   int rc = check_batch(in, out);
   if (rc || in->n == 0) return rc;
-  HIP_TRY(hipSetDevice(ctx->device));
+  gpd::DeviceScope dscope_;
+  HIP_TRY(dscope_.set(ctx->device));
   return launch(ctx, in, out, (hipStream_t)stream, ctx->timing);
 }
 
 int gpd_sync(gpd_ctx *ctx, void *stream) {
   if (!ctx) return set_err(GPD_ERR_INVALID, "gpd_sync: null ctx");
-  HIP_TRY(hipSetDevice(ctx->device));
+  gpd::DeviceScope dscope_;
+  HIP_TRY(dscope_.set(ctx->device));
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
   return GPD_OK;
 }
@@ -748,7 +788,8 @@ int gpd_ip4_fragments(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *res, 
   if (!res->hdr_off || (!res->records && (!res->status || !res->layers)))
     return set_err(GPD_ERR_INVALID, "gpd_ip4_fragments: needs hdr_off and status + layers (or records)");
   if (max_out && !out) return set_err(GPD_ERR_INVALID, "gpd_ip4_fragments: null out with max_out > 0");
-  HIP_TRY(hipSetDevice(ctx->device));
+  gpd::DeviceScope dscope_;
+  HIP_TRY(dscope_.set(ctx->device));
   gpd::FragArgs A{};
   gpd::KParams &P = A.P;
   P.data = in->data;
@@ -908,7 +949,8 @@ int gpd_decode_host(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out) {
   if (in->n > kMaxBatchPackets)
     return set_err(GPD_ERR_INVALID, "gpd_decode_host: batch of %llu packets (max 2^32 - 256)",
                    (unsigned long long)in->n);
-  HIP_TRY(hipSetDevice(ctx->device));
+  gpd::DeviceScope dscope_;
+  HIP_TRY(dscope_.set(ctx->device));
   const uint64_t kPkts = 1u << 20, kBytes = 256ull << 20;
   int rc = alloc_slots(ctx, kBytes, kPkts, out->ext != nullptr, out->detail != nullptr);
   if (rc) return rc;
@@ -1031,7 +1073,8 @@ int gpd_decode_host(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out) {
 // ---- pcap capture in host memory: index, then raw-byte chunks H2D -> decode -> D2H ----
 int gpd_host_register(gpd_ctx *ctx, const void *ptr, uint64_t len) {
   if (!ctx || !ptr || !len) return set_err(GPD_ERR_INVALID, "gpd_host_register: bad argument");
-  HIP_TRY(hipSetDevice(ctx->device));
+  gpd::DeviceScope dscope_;
+  HIP_TRY(dscope_.set(ctx->device));
   HIP_TRY(hipHostRegister(const_cast<void *>(ptr), len, hipHostRegisterDefault));
   ctx->registered.emplace_back((const uint8_t *)ptr, len);
   return GPD_OK;
@@ -1082,7 +1125,8 @@ int gpd_host_unregister(gpd_ctx *ctx, const void *ptr) {
   if (!ctx) return set_err(GPD_ERR_INVALID, "gpd_host_unregister: null ctx");
   for (size_t k = 0; k < ctx->registered.size(); k++) {
     if (ctx->registered[k].first == ptr) {
-      HIP_TRY(hipSetDevice(ctx->device));
+      gpd::DeviceScope dscope_;
+      HIP_TRY(dscope_.set(ctx->device));
       for (auto &s : ctx->slot)
         if (s.stream) HIP_TRY(hipStreamSynchronize(s.stream));
       HIP_TRY(hipHostUnregister(const_cast<void *>(ptr)));
@@ -1483,7 +1527,8 @@ int gpd_decode_pcap_at(gpd_ctx *ctx, const uint8_t *buf, uint64_t len, const gpd
   if (next_pos) *next_pos = pos;
   if (stop) *stop = GPD_PCAP_STOP_LIMIT;
   if (max_n == 0) return GPD_OK;
-  HIP_TRY(hipSetDevice(ctx->device));
+  gpd::DeviceScope dscope_;
+  HIP_TRY(dscope_.set(ctx->device));
   bool dw = ctx->tune.device_walk != 0;
   uint64_t done = 0, at = pos;
   auto shifted = [&](uint64_t d) {
@@ -1601,7 +1646,8 @@ int gpd::decode_tpv3_device(gpd_ctx *ctx, const gpd_tpv3_ring &R, const std::vec
   for (const auto &p : plan)
     if (p.emit > kTwPkts || (p.emit && (p.entry + 48 > B || (p.entry & 15u)))) return GPD_OK;
   if (nthreads <= 0) nthreads = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
-  HIP_TRY(hipSetDevice(ctx->device));
+  gpd::DeviceScope dscope_;
+  HIP_TRY(dscope_.set(ctx->device));
   int rc = alloc_slots(ctx, std::max<uint64_t>(ctx->slot_bytes, kTwGroup),
                        std::max<uint64_t>(ctx->slot_pkts, kTwPkts), false, false);
   if (rc) return rc;

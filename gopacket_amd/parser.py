@@ -111,7 +111,23 @@ class DecodingLayerContainer:
         """layers_decoder.go:11-101: a DecodingLayerFunc over this container's decoders."""
         return DecodingLayerFunc(self, first, df, device)
 
+    def held(self):
+        """Every decoder the container holds (the three containers below enumerate theirs; a
+        user container is probed at the LayerTypes this engine's decoders take)."""
+        for cls in DECODER_BY_NAME.values():
+            for t in cls.can_decode:
+                d, ok = self.Decoder(t)
+                if ok:
+                    yield t, d
+
     def engine_mask(self) -> int:
+        """The decoder kinds to register; a held decoder this engine cannot run (a user-defined
+        DecodingLayer, or one of ours under a LayerType outside its CanDecode) is refused with
+        the TypeError NewDecodingLayerParser raises for it, instead of being dropped silently
+        (its packets would stop with UnsupportedLayerType later)."""
+        for t, d in self.held():
+            if not isinstance(d, DecodingLayer) or not d.bit or t not in d.can_decode:
+                raise TypeError(f"{d!r} (held for LayerType {t}) is not a DecodingLayer this engine implements")
         m = 0
         for cls in DECODER_BY_NAME.values():
             held = [isinstance(self.Decoder(t)[0], cls) for t in cls.can_decode]
@@ -141,6 +157,9 @@ class DecodingLayerSparse(DecodingLayerContainer):
             return self.dl[typ], True
         return None, False
 
+    def held(self):
+        return ((t, d) for t, d in enumerate(self.dl) if d is not None)
+
 
 class DecodingLayerArray(DecodingLayerContainer):
     """parser.go:110-146: (type, decoder) pairs searched linearly; a Put of a type already held
@@ -165,6 +184,9 @@ class DecodingLayerArray(DecodingLayerContainer):
                 return d, True
         return None, False
 
+    def held(self):
+        return ((t, d) for t, d in self.dl)
+
 
 class DecodingLayerMap(DecodingLayerContainer):
     """parser.go:148-169: a map by LayerType (NewDecodingLayerParser's default)."""
@@ -180,6 +202,9 @@ class DecodingLayerMap(DecodingLayerContainer):
     def Decoder(self, typ):
         d = self.dl.get(typ)
         return d, d is not None
+
+    def held(self):
+        return iter(list(self.dl.items()))
 
 
 class DecodingLayerFunc:
@@ -388,8 +413,8 @@ class DecodingLayerParser:
     def SetDecodingLayerContainer(self, dlc: DecodingLayerContainer) -> None:
         """parser.go:236-242: the container's decoders replace the registered set
         (gpd_ctx_set_decoders on an existing context: device and tables kept)."""
-        self._dlc = dlc
-        self._mask = dlc.engine_mask()
+        mask = dlc.engine_mask()  # a container this engine cannot run is refused, parser unchanged
+        self._dlc, self._mask = dlc, mask
 
     def SetTruncated(self) -> None:
         """parser.go:204-209 (DecodeFeedback)."""

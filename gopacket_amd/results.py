@@ -56,7 +56,66 @@ def st_errcode(s):
 
 # ---- Endpoint / Flow (flows.go, layers/endpoints.go:20-35) ----------------------------------
 EndpointIPv4, EndpointIPv6, EndpointTCPPort, EndpointUDPPort = 1, 2, 4, 5
+EndpointMAC, EndpointSCTPPort, EndpointRUDPPort, EndpointUDPLitePort, EndpointPPP = 3, 6, 7, 8, 9
 MaxEndpointSize = 16  # flows.go:27
+# The names the layers package registers (layers/endpoints.go:20-36); EndpointType.String()
+# (flows.go:126-131) prints a registered type's name, else its number.
+ENDPOINT_TYPE_NAMES = {1: "IPv4", 2: "IPv6", 3: "MAC", 4: "TCP", 5: "UDP", 6: "SCTP", 7: "RUDP",
+                       8: "UDPLite", 9: "PPP"}
+
+
+def EndpointTypeString(typ: int) -> str:
+    """EndpointType.String() (flows.go:126-131)."""
+    return ENDPOINT_TYPE_NAMES.get(int(typ), str(int(typ)))
+
+
+_FNV_BASIS, _FNV_PRIME, _M64 = 14695981039346656037, 1099511628211, (1 << 64) - 1
+
+
+def _fnv(raw: bytes) -> int:
+    """fnvHash (flows.go:60-67).  Host arithmetic for ONE caller-built key: the reference's
+    FastHash is a CPU function of a few bytes, and a device launch per key (tens of µs) would
+    make hashing keys in a loop far slower than it; many keys go to the GPU via FastHashes, and
+    decoded packets' hashes come from the decode kernel."""
+    h = _FNV_BASIS
+    for b in raw:
+        h = ((h ^ b) * _FNV_PRIME) & _M64
+    return h
+
+
+def _go_ip_string(b: bytes) -> str:
+    """net.IP(b).String() (Go net/ip.go): dotted quad for 4-byte and IPv4-mapped 16-byte
+    addresses, RFC 5952 hex groups with the first longest run (>1 group) of zeros as '::',
+    '?'+hex for any other length, '<nil>' for none."""
+    if len(b) == 0:
+        return "<nil>"
+    if len(b) == 4 or (len(b) == 16 and b[:10] == bytes(10) and b[10:12] == b"\xff\xff"):
+        return ".".join(str(x) for x in b[-4:])
+    if len(b) != 16:
+        return "?" + b.hex()
+    e0 = e1 = -1
+    i = 0
+    while i < 16:
+        j = i
+        while j < 16 and b[j] == 0 and b[j + 1] == 0:
+            j += 2
+        if j > i and j - i > e1 - e0:
+            e0, e1, i = i, j, j
+        i += 2
+    if e1 - e0 <= 2:
+        e0 = e1 = -1
+    out, i = "", 0
+    while i < 16:
+        if i == e0:
+            out += "::"
+            i = e1
+            if i >= 16:
+                break
+        elif i > 0:
+            out += ":"
+        out += format((b[i] << 8) | b[i + 1], "x")
+        i += 2
+    return out
 
 
 def _device_fast_hash(typs, srcs, dsts=None, device: Optional[int] = None) -> np.ndarray:
@@ -115,18 +174,24 @@ class Endpoint:
     def LessThan(self, b: "Endpoint") -> bool:  # flows.go:53-55
         return self.typ < b.typ or (self.typ == b.typ and self.raw < b.raw)
 
-    def FastHash(self) -> int:  # flows.go:78-83 (on the GPU: gpd_fast_hash)
-        return int(_device_fast_hash([self.typ], [self.raw])[0])
+    def FastHash(self) -> int:  # flows.go:78-83 (one key on the host; FastHashes on the GPU)
+        return ((_fnv(self.raw) ^ (self.typ & _M64)) * _FNV_PRIME) & _M64
 
-    def String(self) -> str:  # layers/endpoints.go:41-95: net.IP / port formatting
-        if self.typ == EndpointIPv4:
-            return ".".join(str(b) for b in self.raw)
-        if self.typ == EndpointIPv6:
-            import ipaddress
-            return str(ipaddress.IPv6Address(self.raw))
-        if self.typ in (EndpointTCPPort, EndpointUDPPort):
-            return str(int.from_bytes(self.raw, "big"))
-        return self.raw.hex()
+    def String(self) -> str:  # layers/endpoints.go:20-36 formatters, else flows.go:133-138
+        t, b = self.typ, self.raw
+        if t in (EndpointIPv4, EndpointIPv6):
+            return _go_ip_string(b)
+        if t == EndpointMAC:  # net.HardwareAddr.String
+            return ":".join(format(x, "02x") for x in b)
+        if t in (EndpointTCPPort, EndpointUDPPort, EndpointSCTPPort, EndpointUDPLitePort):
+            return str(int.from_bytes(b[:2], "big"))  # binary.BigEndian.Uint16
+        if t == EndpointRUDPPort:
+            return str(b[0])
+        if t == EndpointPPP:
+            return "point"
+        # fmt.Sprintf("%v:%v", a.typ, a.raw): raw is the whole [MaxEndpointSize]byte array
+        arr = b + bytes(MaxEndpointSize - len(b))
+        return f"{EndpointTypeString(t)}:[{' '.join(str(x) for x in arr)}]"
 
     __str__ = String
 
@@ -161,8 +226,9 @@ class Flow:
         return Flow(self.typ, self.dst, self.src, self._hash)
 
     def FastHash(self) -> int:  # flows.go:167-174
-        if self._hash is None:  # a caller-built flow: one gpd_fast_hash launch (FastHashes batches)
-            self._hash = int(_device_fast_hash([self.typ], [self.src], [self.dst])[0])
+        if self._hash is None:  # a caller-built flow: host FNV (FastHashes batches on the GPU)
+            h = (_fnv(self.src) + _fnv(self.dst)) & _M64
+            self._hash = ((h ^ (self.typ & _M64)) * _FNV_PRIME) & _M64
         return self._hash
 
     def String(self) -> str:  # flows.go:207-212
@@ -194,7 +260,8 @@ def NewFlow(typ: int, src: bytes, dst: bytes) -> Flow:
 def FlowFromEndpoints(src: Endpoint, dst: Endpoint):
     """flows.go:151-157: (Flow, None), or (an empty Flow, the error) for mismatched types."""
     if src.typ != dst.typ:
-        return Flow(0, b"", b""), ValueError(f"Mismatched endpoint types: {src.typ}->{dst.typ}")
+        return Flow(0, b"", b""), ValueError(
+            f"Mismatched endpoint types: {EndpointTypeString(src.typ)}->{EndpointTypeString(dst.typ)}")
     return Flow(src.typ, src.raw, dst.raw), None
 
 

@@ -106,6 +106,8 @@ extern "C" {
 #define GPD_OPT_IGNORE_PANIC       (1u << 1)  /* accepted; no decoder here can panic */
 #define GPD_OPT_NO_CHECKSUMS       (1u << 8)  /* skip IPv4-header and L4 checksums (csum := 0, valid bits 0) */
 #define GPD_OPT_NO_FLOW_HASH       (1u << 9)  /* skip FastHash (hashes := 0, valid bits 0) */
+/* Every other bit is unknown: gpd_ctx_create and gpd_ctx_set_options return GPD_ERR_INVALID for
+ * it (the bench's stream-only ablations live in a separately built diagnostic library). */
 
 /* ---- per-packet status word (uint32) ----
  *  [1:0]   class: GPD_ST_OK (DecodeLayers returned nil), GPD_ST_UNSUPPORTED

@@ -371,9 +371,21 @@ static int check_reconfig(const gpd_config *base, const uint8_t *data, uint64_t 
   CHECK(gpd_ctx_reload_tables(ctx, &cfg));
   CHECK(gpd_ctx_add_decoders(ctx, base->decoders & GPD_DEC_VXLAN));
   int bad = 0;
-  if (gpd_ctx_set_options(ctx, 1u << 26) != GPD_ERR_INVALID) {
-    fprintf(stderr, "reconfig: internal option bits accepted\n");
-    bad = 1;
+  /* every bit outside the four GPD_OPT_* is refused: the runtime's launch flags (24-29) and the
+   * diagnostic library's ablation bits (30: no DMA wait, 31: no decode) included */
+  for (int b = 0; b < 32; b++) {
+    const uint32_t bit = 1u << b;
+    if (bit & (GPD_OPT_IGNORE_UNSUPPORTED | GPD_OPT_IGNORE_PANIC | GPD_OPT_NO_CHECKSUMS | GPD_OPT_NO_FLOW_HASH))
+      continue;
+    gpd_config bc = *base;
+    gpd_ctx *bx = NULL;
+    bc.options = base->options | bit;
+    if (gpd_ctx_set_options(ctx, base->options | bit) != GPD_ERR_INVALID ||
+        gpd_ctx_create(0, &bc, &bx) != GPD_ERR_INVALID || bx != NULL) {
+      fprintf(stderr, "reconfig: option bit %d accepted\n", b);
+      if (bx) gpd_ctx_destroy(bx);
+      bad = 1;
+    }
   }
   res_t hv = res_alloc(n), dv = res_alloc(n), ov = res_alloc(n);
   gpd_ext_rec *oext = calloc(n + 1, sizeof(gpd_ext_rec));

@@ -198,3 +198,16 @@ def test_fast_kernels_do_not_spill():
         spill = int(re.search(r"\.vgpr_spill_count:\s+(\d+)", b).group(1))
         assert spill == 0, f"{name}: {spill} VGPRs spilled"
     assert seen >= 30
+
+
+def test_shipped_library_has_no_diagnostic_kernels():
+    """the shipped libgpd.so instantiates every fast kernel without the skeleton
+    diagnostic (rs_kernel's last template argument, DIAG, false), the config-2 4 KiB kernel
+    included; only libgpd_diag.so (-DGPD_DIAG, bench --ablate) carries DIAG=true kernels."""
+    lib = os.path.join(ROOT, "gopacket_amd", "libgpd.so")
+    out = subprocess.run(["nm", "-C", lib], check=True, capture_output=True, text=True).stdout
+    inst = set(re.findall(r"rs_kernel<([^>]*)>", out))
+    assert len(inst) >= 30, inst
+    diag = [a for a in inst if a.split(",")[-1].strip() == "true"]
+    assert not diag, diag
+    assert any(a.replace(" ", "").startswith("4096,true,true,4,") for a in inst)

@@ -63,7 +63,108 @@ def test_endpoint_and_flow_constructors():
     assert err is None and f.Src() == a and f.Dst() == b and f.String() == "10.0.0.1->10.0.0.2"
     assert f.Reverse().Src() == b and f.Reverse().Reverse() == f
     _, err = FlowFromEndpoints(a, NewEndpoint(EndpointTCPPort, b"\x00\x50"))
-    assert str(err) == "Mismatched endpoint types: 1->4"
+    assert str(err) == "Mismatched endpoint types: IPv4->TCP"  # EndpointType.String, flows.go:126-131
+    _, err = FlowFromEndpoints(NewEndpoint(1000, b"x"), a)
+    assert str(err) == "Mismatched endpoint types: 1000->IPv4"
     assert a.LessThan(b) and not b.LessThan(a) and not a.LessThan(a)
     assert b.LessThan(NewEndpoint(EndpointTCPPort, b"\x00\x01"))  # type first
     assert NewEndpoint(EndpointIPv4, b"\x0a").LessThan(a)  # a prefix sorts first (bytes.Compare)
+
+
+def test_endpoint_strings_follow_the_registered_formatters():
+    """layers/endpoints.go:20-36 formatters (net.IP, net.HardwareAddr, big-endian ports, RUDP's
+    one byte, PPP's "point") and flows.go:133-138's fallback "%v:%v" of the type and the whole
+    [MaxEndpointSize]byte array for unregistered types.  Go's net.IP.String prints IPv4-mapped
+    IPv6 addresses as a dotted quad and compresses the first longest run of two or more zero
+    groups (parity unpinned: no reference fixture holds these strings; restated from Go's
+    net/ip.go)."""
+    from gopacket_amd.results import NewEndpoint, NewFlow
+    ip6 = bytes.fromhex
+    cases = [
+        (1, bytes([192, 168, 1, 2]), "192.168.1.2"),
+        (2, ip6("00000000000000000000ffff0a000001"), "10.0.0.1"),
+        (2, ip6("20010db8000000000000000000000001"), "2001:db8::1"),
+        (2, ip6("20010db8000000010000000000000001"), "2001:db8:0:1::1"),
+        (2, ip6("20010db8000100000001000000000000"), "2001:db8:1:0:1::"),
+        (2, ip6("20010db8000000010000000100000001"), "2001:db8:0:1:0:1:0:1"),
+        (2, bytes(16), "::"),
+        (2, ip6("00000000000000000000000000000001"), "::1"),
+        (2, ip6("fe800000000000000202b3fffe1e8329"), "fe80::202:b3ff:fe1e:8329"),
+        (3, bytes([0, 0x1b, 0x21, 0xaa, 0xbb, 0x0c]), "00:1b:21:aa:bb:0c"),
+        (4, b"\x01\xbb", "443"), (5, b"\x12\xb5", "4789"), (6, b"\x00\x50", "80"),
+        (7, b"\x07", "7"), (8, b"\x00\x35", "53"), (9, b"", "point"),
+        (1000, b"\x01\x02", "1000:[1 2 0 0 0 0 0 0 0 0 0 0 0 0 0 0]"),
+    ]
+    for t, raw, want in cases:
+        assert NewEndpoint(t, raw).String() == want, (t, raw, want)
+    f = NewFlow(2, ip6("00000000000000000000ffff0a000001"), ip6("20010db8000000000000000000000001"))
+    assert f.String() == "10.0.0.1->2001:db8::1"
+
+
+def test_single_key_fast_hash_on_the_host():
+    """Flow.FastHash / Endpoint.FastHash of ONE caller-built key is host FNV
+    (flows.go:60-83,167-174), as the reference's ~10-ns CPU function is — no device launch —
+    equal to the oracle's FNV for every key of the GPU test
+    test_fast_hash_of_built_flows_and_endpoints (raw lengths 0..16, types beyond 32 bits and
+    negative), symmetric under Reverse()."""
+    import numpy as np
+    import oracle_ref as O
+    from gopacket_amd import results as R
+    ol = O.lib()
+    M = (1 << 64) - 1
+
+    def ofnv(b):
+        return int(ol.gpo_fnv_hash(bytes(b), len(b)))
+
+    called = []
+    saved = R._device_fast_hash
+    R._device_fast_hash = lambda *a, **k: called.append(1)
+    try:
+        rng = np.random.default_rng(9)
+        typs = [1, 2, 4, 5, 1000, 77777, (1 << 40) + 3, -5, 0]
+        for k in range(600):
+            t = typs[k % len(typs)]
+            a = rng.integers(0, 256, int(rng.integers(0, 17)), dtype=np.uint8).tobytes()
+            b = rng.integers(0, 256, int(rng.integers(0, 17)), dtype=np.uint8).tobytes()
+            want_f = ((((ofnv(a) + ofnv(b)) & M) ^ (t & M)) * 1099511628211) & M
+            want_e = ((ofnv(a) ^ (t & M)) * 1099511628211) & M
+            f = R.NewFlow(t, a, b)
+            assert f.FastHash() == want_f and f.Reverse().FastHash() == want_f
+            assert R.NewFlow(t, b, a).FastHash() == want_f
+            assert R.NewEndpoint(t, a).FastHash() == want_e
+            if 0 <= t < (1 << 32):
+                assert want_f == ol.gpo_flow_fasthash(t, a, len(a), b, len(b))
+                assert want_e == ol.gpo_endpoint_fasthash(t, a, len(a))
+    finally:
+        R._device_fast_hash = saved
+    assert not called, "a single key launched the device"
+
+
+def test_container_with_a_decoder_the_engine_cannot_run_is_refused():
+    """SetDecodingLayerContainer refuses a container holding a decoder the engine
+    cannot run (a user-defined DecodingLayer for TCP or for a type outside the engine's set), as
+    NewDecodingLayerParser does, instead of dropping it; the parser keeps its previous set."""
+    import pytest
+    from gopacket_amd import parser as P
+
+    class UserTCP:  # a caller's own DecodingLayer (CanDecode TCP)
+        def CanDecode(self):
+            return (L.LayerTypeTCP,)
+
+    class UserDNS:
+        def CanDecode(self):
+            return (53,)
+
+    p = P.DecodingLayerParser(L.LayerTypeEthernet, P.Ethernet(), P.IPv4(), P.TCP())
+    before = p.decoders
+    for c in (P.DecodingLayerSparse, P.DecodingLayerArray, P.DecodingLayerMap):
+        for bad in (UserTCP(), UserDNS()):
+            dlc = c().Put(P.Ethernet()).Put(P.IPv4()).Put(bad)
+            with pytest.raises(TypeError, match="not a DecodingLayer this engine implements"):
+                p.SetDecodingLayerContainer(dlc)
+            assert p.decoders == before
+        ok = c().Put(P.Ethernet()).Put(P.IPv6())
+        p.SetDecodingLayerContainer(ok)
+        assert p.decoders == P.DEC_ETHERNET | P.DEC_IPV6
+        p.SetDecodingLayerContainer(c().Put(P.Ethernet()).Put(P.IPv4()).Put(P.TCP()))
+        assert p.decoders == before

@@ -7,6 +7,8 @@ BASELINE configurations, exhaustive truncations and seeded byte mutations of the
 golden packets, odd batch layouts (unaligned / shuffled offsets, packets larger
 than an LDS window, empty packets) and mutated dispatch tables.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -554,6 +556,33 @@ def test_reconfigure_in_place_keeps_tables_and_context():
             assert p.ctx().h.value == h, "the context was re-created"
     finally:
         L.TABLES.udp_port[:] = saved.udp_port
+
+
+def test_option_bits_outside_the_header_are_refused():
+    """include/gpd.h: the reference has two options (parser.go:336-350), the engine two more;
+    every other bit — the runtime's launch flags (24-29) and the ablation bits 30 (no DMA wait)
+    and 31 (no decode), which only the diagnostic library takes — is GPD_ERR_INVALID from
+    gpd_ctx_set_options and gpd_ctx_create, and a refused bit leaves the context's options as
+    they were (its next decode equals the oracle)."""
+    import ctypes as C
+    from gopacket_amd import parser as P
+    from gopacket_amd._lib import GPD_ERR_INVALID, GpdConfig, lib
+    assert os.path.basename(P.lib._name) == "libgpd.so"
+    p = _parser()
+    b = PacketBatch.from_packets(_golden_packets())
+    p.DecodeBatch(b)
+    h = p.ctx().h
+    known = P.OPT_IGNORE_UNSUPPORTED | P.OPT_IGNORE_PANIC | P.OPT_NO_CHECKSUMS | P.OPT_NO_FLOW_HASH
+    for bit in range(32):
+        if (1 << bit) & known:
+            continue
+        assert lib.gpd_ctx_set_options(h, p.options | (1 << bit)) == GPD_ERR_INVALID, bit
+        cfg = GpdConfig(L.LayerTypeEthernet, p.decoders, 1 << bit, 0, None, None, None, None)
+        out = C.c_void_p()
+        assert lib.gpd_ctx_create(0, C.byref(cfg), C.byref(out)) == GPD_ERR_INVALID, bit
+        assert not out.value
+    ref = O.decode(b, L.LayerTypeEthernet, p.decoders, p.options, ext=False)
+    assert_same(p.DecodeBatch(b), ref, b, False)
 
 
 def test_set_decoding_layer_container_in_place():
