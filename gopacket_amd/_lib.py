@@ -17,7 +17,7 @@ DIAG_LIB_PATH = os.path.join(_HERE, "libgpd_diag.so")
 if os.environ.get("GPD_DIAGNOSTIC_LIBRARY") == "1":
     LIB_PATH = DIAG_LIB_PATH
 
-GPD_ABI_VERSION = 9
+GPD_ABI_VERSION = 10
 GPD_OK = 0
 GPD_ERR_INVALID = -1
 
@@ -42,7 +42,7 @@ class GpdResult(C.Structure):
 class GpdTuning(C.Structure):
     _fields_ = [("window_bytes", C.c_uint32), ("shift", C.c_int32), ("reg_prefix", C.c_int32),
                 ("waves_per_simd", C.c_int32), ("header_once", C.c_int32),
-                ("device_walk", C.c_int32)]
+                ("device_walk", C.c_int32), ("grid_rounds", C.c_int32)]
 
 
 class GpdPcapInfo(C.Structure):

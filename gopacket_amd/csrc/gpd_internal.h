@@ -92,6 +92,7 @@ struct KParams {
   uint32_t nstores;            // store instructions per tile (non-NULL result arrays)
   uint32_t fixed;              // tables in the kFix* layout (eth_mult shared by all three)
   uint32_t waves;              // fast kernel waves per SIMD (0: the default for the window)
+  uint32_t rounds;             // fast kernel grid rounds of resident workgroups (0: the default)
   uint64_t *fb_list;           // fast kernel: packets left to the generic decoder (offset << 32 |
                                // index: the decode's loads skip the descriptor), in one private
                                // region per wave (64 x its tiles), which that wave decodes after
@@ -101,7 +102,7 @@ struct KParams {
 };
 // Upper bound of the fast kernel's waves per launch, per compute unit (workgroups per CU x
 // grid rounds x 4 waves): sizes fb_wcount.
-constexpr uint32_t kMaxFastWavesPerCU = 4 * 4 * 4;
+constexpr uint32_t kMaxFastWavesPerCU = 4 * 8 * 4;
 
 // True when launch_decode takes the fast kernel (needs fb_list with room for P.n entries and
 // fb_wcount).

@@ -2485,14 +2485,21 @@ template <int STAGE, bool CS, bool HASH, int MINW, bool DEFER = false, bool RPFX
           bool AL = false, bool DIAG = false>
 static hipError_t launch_rs(KParams &P, hipStream_t stream, int num_cus) {
   const uint64_t ntiles = (P.n + 63) / 64;
-  const size_t lds = ((P.image_words * 4u + 15u) & ~15u) + 4 * (size_t)rs_wave_lds_bytes(STAGE) + 64;
-  const uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>((160u * 1024u) / lds, MINW));
+  size_t lds = ((P.image_words * 4u + 15u) & ~15u) + 4 * (size_t)rs_wave_lds_bytes(STAGE) + 64;
+  uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>((160u * 1024u) / lds, MINW));
+  // gpd_tuning.waves_per_simd: at most that many workgroups per CU, by reserving 1/W of the
+  // CU's LDS per workgroup (the kernel's registers alone would admit 4)
+  if (P.waves) {
+    lds = std::max<size_t>(lds, ((160u * 1024u) / P.waves) & ~(size_t)2047u);  // (LDS granules: 3 x 54,608 B do not fit)
+    per_cu = std::max<uint64_t>(1, std::min<uint64_t>((160u * 1024u) / lds, P.waves));
+  }
   uint64_t blocks = (ntiles + 3) / 4;
   // rounds of resident workgroups: the AL kernel (VXLAN-sized frames) runs one — each wave's
   // tiles four times longer — measured 2.2 % faster than four (and 1.6 % than two) on config
   // 4; config 2, IMIX, pcap64 and the traffic mix keep four (one: +1-2 %, two: within noise;
   // tools/ab_rounds.sh, profiles/r03/rounds_ab/)
-  const uint64_t cap = (uint64_t)num_cus * per_cu * (AL ? 1u : kGridRounds);
+  const uint64_t rounds = P.rounds ? P.rounds : (AL ? 1u : kGridRounds);
+  const uint64_t cap = (uint64_t)num_cus * per_cu * rounds;
   if (blocks > cap) blocks = cap;
   P.fb_waves = (uint32_t)blocks * 4u;
   if (blocks == 0) return hipSuccess;
@@ -2508,10 +2515,14 @@ static hipError_t launch_rs(KParams &P, hipStream_t stream, int num_cus) {
 template <bool CS, bool HASH, int MINW>
 static hipError_t launch_ro(KParams &P, hipStream_t stream, int num_cus) {
   const uint64_t ntiles = (P.n + 63) / 64;
-  const size_t lds = ((P.image_words * 4u + 15u) & ~15u) + 4 * (size_t)ro_wave_lds_bytes() + 64;
-  const uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>((160u * 1024u) / lds, MINW));
+  size_t lds = ((P.image_words * 4u + 15u) & ~15u) + 4 * (size_t)ro_wave_lds_bytes() + 64;
+  uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>((160u * 1024u) / lds, MINW));
+  if (P.waves) {  // (as launch_rs: the LDS reservation caps the resident workgroups per CU)
+    lds = std::max<size_t>(lds, ((160u * 1024u) / P.waves) & ~(size_t)2047u);  // (LDS granules: 3 x 54,608 B do not fit)
+    per_cu = std::max<uint64_t>(1, std::min<uint64_t>((160u * 1024u) / lds, P.waves));
+  }
   uint64_t blocks = (ntiles + 3) / 4;
-  const uint64_t cap = (uint64_t)num_cus * per_cu * kGridRounds;
+  const uint64_t cap = (uint64_t)num_cus * per_cu * (P.rounds ? P.rounds : kGridRounds);
   if (blocks > cap) blocks = cap;
   P.fb_waves = (uint32_t)blocks * 4u;
   if (blocks == 0) return hipSuccess;
@@ -2522,17 +2533,15 @@ static hipError_t launch_ro(KParams &P, hipStream_t stream, int num_cus) {
 
 template <bool CS, bool HASH>
 static hipError_t launch_fast(KParams &P, hipStream_t stream, int num_cus) {
-  if (P.options & kRounds) {  // header-once over 8 KiB rounds of each tile's run (ro_kernel)
-    if (P.waves == 2) return launch_ro<CS, HASH, 2>(P, stream, num_cus);
+  // One register budget per kernel (4 waves per SIMD for 4 KiB windows, 3 for 8 KiB windows
+  // and rounds: what each kernel's VGPRs admit without spills); gpd_tuning.waves_per_simd caps
+  // the residency below that through the LDS reservation (launch_rs / launch_ro), it does not
+  // pick another instantiation.
+  if (P.options & kRounds)  // header-once over 8 KiB rounds of each tile's run (ro_kernel)
     return launch_ro<CS, HASH, 3>(P, stream, num_cus);
-  }
   if constexpr (kDiagBuild) {  // libgpd_diag.so: the skeleton (no decode) instantiations
     if (P.options & kDiagSkipDecode) {
-      if (P.stage == 4096) {
-        if (P.waves == 2) return launch_rs<4096, CS, HASH, 2, false, true, false, false, true>(P, stream, num_cus);
-        if (P.waves == 3) return launch_rs<4096, CS, HASH, 3, false, true, false, false, true>(P, stream, num_cus);
-        return launch_rs<4096, CS, HASH, 4, false, true, false, false, true>(P, stream, num_cus);
-      }
+      if (P.stage == 4096) return launch_rs<4096, CS, HASH, 4, false, true, false, false, true>(P, stream, num_cus);
       if (P.options & kHeaderOnce) return launch_rs<8192, CS, HASH, 3, false, true, true, false, true>(P, stream, num_cus);
       if (P.options & kRegPrefix) return launch_rs<8192, CS, HASH, 3, false, true, false, false, true>(P, stream, num_cus);
       if (!(P.options & kShiftWindows))
@@ -2540,16 +2549,8 @@ static hipError_t launch_fast(KParams &P, hipStream_t stream, int num_cus) {
       return launch_rs<8192, CS, HASH, 3, false, false, false, false, true>(P, stream, num_cus);
     }
   }
-  if (P.stage == 4096) {
-    if (P.waves == 2) return launch_rs<4096, CS, HASH, 2>(P, stream, num_cus);
-    if (P.waves == 3) return launch_rs<4096, CS, HASH, 3>(P, stream, num_cus);
-    return launch_rs<4096, CS, HASH, 4>(P, stream, num_cus);
-  }
-  if (P.options & kHeaderOnce) {
-    if (P.waves == 2) return launch_rs<8192, CS, HASH, 2, false, true, true>(P, stream, num_cus);
-    return launch_rs<8192, CS, HASH, 3, false, true, true>(P, stream, num_cus);
-  }
-  if (P.waves == 2) return launch_rs<8192, CS, HASH, 2>(P, stream, num_cus);
+  if (P.stage == 4096) return launch_rs<4096, CS, HASH, 4>(P, stream, num_cus);
+  if (P.options & kHeaderOnce) return launch_rs<8192, CS, HASH, 3, false, true, true>(P, stream, num_cus);
   if (P.options & kRegPrefix) return launch_rs<8192, CS, HASH, 3>(P, stream, num_cus);
   // unshifted windows of mid-sized frames (VXLAN's 128 B): the aligned-chunk transport checksum
   // and the inner Ethernet bytes from registers (fast_decode AL); shifted windows (pcap records,

@@ -578,7 +578,7 @@ int gpd_last_launch_split(gpd_ctx *ctx, uint64_t *fallback, float *fast_ms, floa
 
 int gpd_ctx_set_tuning(gpd_ctx *ctx, const gpd_tuning *t) {
   if (!ctx) return set_err(GPD_ERR_INVALID, "gpd_ctx_set_tuning: null ctx");
-  const gpd_tuning automatic{0, -1, -1, 0, -1, -1};  // (waves_per_simd 0: automatic)
+  const gpd_tuning automatic{0, -1, -1, 0, -1, -1, 0};  // (waves_per_simd 0: automatic)
   if (!t) t = &automatic;
   if (t->window_bytes != 0 && t->window_bytes != 4096 && t->window_bytes != 8192)
     return set_err(GPD_ERR_INVALID, "gpd_ctx_set_tuning: window_bytes %u (0, 4096 or 8192)", t->window_bytes);
@@ -589,6 +589,8 @@ int gpd_ctx_set_tuning(gpd_ctx *ctx, const gpd_tuning *t) {
                    "outside {-1, 0, 1, 2}");
   if (t->waves_per_simd != 0 && (t->waves_per_simd < 2 || t->waves_per_simd > 4))
     return set_err(GPD_ERR_INVALID, "gpd_ctx_set_tuning: waves_per_simd %d (0, 2, 3 or 4)", t->waves_per_simd);
+  if (t->grid_rounds < 0 || t->grid_rounds > 8)
+    return set_err(GPD_ERR_INVALID, "gpd_ctx_set_tuning: grid_rounds %d (0 .. 8)", t->grid_rounds);
   ctx->tune = *t;
   return GPD_OK;
 }
@@ -696,6 +698,7 @@ static int launch(gpd_ctx *ctx, const gpd_batch *in, const gpd_result *out, hipS
   if (P.stage == 8192 && ho == 1) P.options |= 1u << 25;
   if (ho == 2) P.options |= 1u << 24;
   P.waves = (uint32_t)ctx->tune.waves_per_simd;
+  P.rounds = (uint32_t)ctx->tune.grid_rounds;
   P.nstores = out->records ? 2u + (out->hdr_off != nullptr)
                            : 2u + (out->net_hash != nullptr) + (out->tp_hash != nullptr) +
                                  (out->csum != nullptr) + (out->hdr_off != nullptr);

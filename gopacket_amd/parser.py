@@ -456,17 +456,18 @@ class DecodingLayerParser:
 
     # Engine tuning (gpd_ctx_set_tuning): staging choices that never change a result.
     # Keys: window_bytes (0 auto / 4096 / 8192), shift and reg_prefix (-1 auto / 0 / 1),
-    # waves_per_simd (0 auto / 2 / 3 / 4), header_once (-1 auto / 0 / 1 windows / 2 rounds) and
-    # device_walk (-1 auto / 0 / 1).
+    # waves_per_simd (0 auto / 2 / 3 / 4), header_once (-1 auto / 0 / 1 windows / 2 rounds),
+    # device_walk (-1 auto / 0 / 1) and grid_rounds (0 auto / 1..8).
     Tuning: Optional[dict] = None
 
     def _apply_tuning(self):
         from ._lib import GpdTuning
         t = dict(window_bytes=0, shift=-1, reg_prefix=-1, waves_per_simd=0, header_once=-1,
-                 device_walk=-1)
+                 device_walk=-1, grid_rounds=0)
         t.update(self.Tuning or {})
         g = GpdTuning(int(t["window_bytes"]), int(t["shift"]), int(t["reg_prefix"]),
-                      int(t["waves_per_simd"]), int(t["header_once"]), int(t["device_walk"]))
+                      int(t["waves_per_simd"]), int(t["header_once"]), int(t["device_walk"]),
+                      int(t["grid_rounds"]))
         check(lib.gpd_ctx_set_tuning(self._ctx.h, C.byref(g)), "gpd_ctx_set_tuning")
         self._ctx.tuned = dict(self.Tuning) if self.Tuning else None
 

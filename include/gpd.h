@@ -50,14 +50,14 @@
 extern "C" {
 #endif
 
-#define GPD_ABI_VERSION 9  /* 2: ICMPv4 + LLC, 12 objects, 224-B ext; 3: gpd_result.hdr_off;
+#define GPD_ABI_VERSION 10 /* 2: ICMPv4 + LLC, 12 objects, 224-B ext; 3: gpd_result.hdr_off;
                               4: gpd_ctx_set_tuning; 5: gpd_tuning.header_once,
                               gpd_tuning.device_walk, gpd_result.records; 6: outputs follow the
                               objects as a failing call leaves them; ext err_obj/err_wrote/err_off;
                               7: gpd_result.detail (error arguments and deep stacks without ext);
                               8: gpd_ctx_set_options, gpd_ctx_add_decoders, gpd_ctx_set_decoders
                               (in place: device, tables and staging kept); 9: gpd_fast_hash
-                              (gpd_flow.h) */
+                              (gpd_flow.h); 10: gpd_tuning.grid_rounds, waves_per_simd enforced */
 
 /* ---- gopacket LayerType numbers (layertypes.go:14-154, decode.go:105-116) ---- */
 #define GPD_LT_ZERO            0
@@ -411,8 +411,9 @@ typedef struct gpd_tuning {
                              -1 automatic (mean slot <= 96 B), 0 off, 1 on */
   int32_t  reg_prefix;    /* 8 KiB windows' chunk prefix sums from the registers at commit:
                              -1 automatic (mean slot > 160 B), 0 off, 1 on */
-  int32_t  waves_per_simd; /* resident waves of the fast kernel per SIMD: 0 automatic, 2, 3, 4
-                              (4 KiB windows) or 2, 3 (8 KiB windows) */
+  int32_t  waves_per_simd; /* resident waves of the fast kernel per SIMD (= its 4-wave workgroups
+                              per CU), enforced by the workgroup's LDS reservation: 0 automatic,
+                              2, 3, 4 (4 KiB windows) or 2, 3 (8 KiB windows) */
   int32_t  header_once;   /* decode each 64-packet tile once from headers staged as its bytes
                              pass, instead of once per window: 0 off, 1 over 8 KiB windows cut at
                              packet boundaries, 2 over 8 KiB rounds of the tile's contiguous byte
@@ -421,6 +422,8 @@ typedef struct gpd_tuning {
   int32_t  device_walk; /* gpd_decode_pcap(_at): find the records in HBM after the raw
                                bytes arrive (gpd_pcapwalk.hip) instead of walking them on the
                                host first: -1 automatic (on), 0 off, 1 on */
+  int32_t  grid_rounds; /* ABI 10: the fast kernel's grid in rounds of resident workgroups
+                           (each wave takes every (grid waves)-th tile): 0 automatic, 1..8 */
 } gpd_tuning;
 int  gpd_ctx_set_tuning(gpd_ctx *ctx, const gpd_tuning *t);
 const char *gpd_last_error_string(void);

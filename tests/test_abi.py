@@ -39,7 +39,7 @@ def test_library_exports_every_declared_symbol():
     lib = C.CDLL(_lib.LIB_PATH)
     missing = [f for f in declared_functions() if not hasattr(lib, f)]
     assert not missing, missing
-    assert lib.gpd_abi_version() == 9
+    assert lib.gpd_abi_version() == 10
 
 
 def test_python_binding_covers_the_header():
@@ -197,7 +197,7 @@ def test_fast_kernels_do_not_spill():
         seen += 1
         spill = int(re.search(r"\.vgpr_spill_count:\s+(\d+)", b).group(1))
         assert spill == 0, f"{name}: {spill} VGPRs spilled"
-    assert seen >= 30
+    assert seen >= 20
 
 
 def test_shipped_library_has_no_diagnostic_kernels():
@@ -207,7 +207,7 @@ def test_shipped_library_has_no_diagnostic_kernels():
     lib = os.path.join(ROOT, "gopacket_amd", "libgpd.so")
     out = subprocess.run(["nm", "-C", lib], check=True, capture_output=True, text=True).stdout
     inst = set(re.findall(r"rs_kernel<([^>]*)>", out))
-    assert len(inst) >= 30, inst
+    assert len(inst) >= 20, inst
     diag = [a for a in inst if a.split(",")[-1].strip() == "true"]
     assert not diag, diag
     assert any(a.replace(" ", "").startswith("4096,true,true,4,") for a in inst)

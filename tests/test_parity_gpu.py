@@ -494,6 +494,24 @@ def test_vxlan_frame_shapes_in_every_kernel(align):
     run_both(b, mask=0x3FF, options=1, ext=False, tuning=dict(header_once=2))
 
 
+@pytest.mark.parametrize("geom", [dict(waves_per_simd=2, grid_rounds=1), dict(waves_per_simd=3, grid_rounds=2),
+                                  dict(waves_per_simd=4, grid_rounds=8), dict(grid_rounds=1)],
+                         ids=["w2r1", "w3r2", "w4r8", "r1"])
+def test_launch_geometry_never_changes_results(geom):
+    """gpd_tuning.waves_per_simd (now enforced: an LDS reservation of 1/W of the CU per
+    workgroup) and grid_rounds (ABI 10) change only how many waves stream and how many tiles
+    each takes, through every fast kernel (4 KiB windows shifted, 8 KiB AL / plain / header-once
+    windows, rounds) with fallback lists, against the oracle; with more tiles than one round of
+    waves and with fewer."""
+    mixed = synth.make_mixed(6000)
+    golden = PacketBatch.from_packets(_golden_packets() * 7)
+    cases = [(synth.make_udp64(40000), {}), (synth.make_vxlan(20000), {}), (synth.make_imix(12000), {}),
+             (mixed, {}), (mixed, dict(window_bytes=8192, header_once=1)),
+             (golden, dict(window_bytes=4096)), (synth.make_udp64(3000), {})]
+    for b, t in cases:
+        run_both(b, ext=False, tuning=dict(t, **geom))
+
+
 def test_layouts_unaligned_shuffled_large_empty():
     pk = _golden_packets() + [b"", b"\x01", b"\x00" * 13]
     big = [G.case_bytes(c) for c in CASES if c["name"] == "ipv6_jumbogram_dlp"][0]
