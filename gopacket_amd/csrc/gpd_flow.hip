@@ -241,12 +241,25 @@ __device__ __forceinline__ void add_run(FlowHot &r, FlowCold &cr, uint64_t mn, u
   if (spill) atomicAdd(reinterpret_cast<unsigned long long *>(&cr.spill), (unsigned long long)spill);
 }
 
-// Is the record's stored key the packet's key?
+// Is the record's stored key the packet's key?  The key's 40 bytes (record bytes 8..47) as one
+// 8-byte and two 16-byte loads issued together, compared branch-free: a short-circuit `&&`
+// compiled to eight dependent load-wait-compare steps per packet of an existing flow
+// (round 6: 0.9 ms of the 2.43-ms existing-flow insert, tools/flow_prof.sh).
+struct StoredKey {
+  uint2 a;
+  uint4 b, c;
+};
+__device__ __forceinline__ StoredKey load_key(const FlowHot &r) {
+  return StoredKey{*reinterpret_cast<const uint2 *>(&r.key[0]), *reinterpret_cast<const uint4 *>(&r.key[2]),
+                   *reinterpret_cast<const uint4 *>(&r.key[6])};
+}
+__device__ __forceinline__ bool key_eq(const StoredKey &r, const uint32_t (&k)[10]) {
+  const uint32_t d = (r.a.x ^ k[0]) | (r.a.y ^ k[1]) | (r.b.x ^ k[2]) | (r.b.y ^ k[3]) | (r.b.z ^ k[4]) |
+                     (r.b.w ^ k[5]) | (r.c.x ^ k[6]) | (r.c.y ^ k[7]) | (r.c.z ^ k[8]) | (r.c.w ^ k[9]);
+  return d == 0u;
+}
 __device__ __forceinline__ bool same_key(const FlowHot &r, const uint32_t (&k)[10]) {
-  bool same = true;
-#pragma unroll
-  for (int j = 0; j < 10; j++) same = same && r.key[j] == k[j];
-  return same;
+  return key_eq(load_key(r), k);
 }
 
 // Sequence number and captured length of item i.
@@ -341,6 +354,11 @@ __global__ __launch_bounds__(kFlowThreads) void flow_insert_kernel(FlowParams P)
     const uint64_t done = __ballot(created || (pre && keyed && !full));
     if (lane == 0u && i < P.n) P.made[i >> 6] = done;  // i = the wave's first packet
     const bool counted = keyed && !full;
+    // the key check of a record an earlier launch published: its loads issued ahead of the
+    // counter atomics (in flight together), the compare after them
+    const bool chk = counted && pre;
+    StoredKey rk{};
+    if (chk) rk = load_key(P.tab[s]);
     uint64_t mn = seq, mx = seq, pb = (1ull << kPktShift) | caplen;
     uint32_t start;
     const bool tail = fold_run(counted, s, mn, mx, pb, start);
@@ -348,8 +366,7 @@ __global__ __launch_bounds__(kFlowThreads) void flow_insert_kernel(FlowParams P)
       if ((made >> start) & 1ull) store_run(P.tab[s], P.cold[s], mn, mx, pb, P.cbits);
       else if (pre) add_run(P.tab[s], P.cold[s], mn, mx, pb, P.cbits, mn >= P.seen);
     }
-    bool bad = false;
-    if (counted && pre) bad = !same_key(P.tab[s], k);
+    const bool bad = chk && !key_eq(rk, k);
     if (bad) P.flow_id[i] = (uint32_t)s | GPD_FLOW_COLLISION;
     if (live && !bad) P.flow_id[i] = !keyed ? GPD_FLOW_NONE : full ? GPD_FLOW_FULL : (uint32_t)s;
     wave_tally(t_coll, bad);

@@ -119,6 +119,47 @@ __global__ __launch_bounds__(256) void reg_k(const uint8_t *__restrict__ data, c
   }
 }
 
+
+// Two of the wave's tiles per iteration (tiles t and t + nw: two 4 KiB windows, 8 register chunks
+// per lane), one pair in flight: twice the bytes per wave-iteration of reg_k.
+template <int SPIN>
+__global__ __launch_bounds__(256) void reg2_k(const uint8_t *__restrict__ data, const uint32_t *__restrict__ off,
+                                              const uint32_t *__restrict__ cap, v4u *rec, uint32_t ntiles) {
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint32_t nw = gridDim.x * 4u;
+  const uint32_t buf = wave * 8192u;
+  uint32_t t = blockIdx.x * 4u + wave;
+  if (t >= ntiles) return;
+  v4u wv[8];
+  auto wl = [&](uint32_t u) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const uint32_t uu = u + (j >> 2) * nw;
+      wv[j] = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(data + (uint64_t)(uu < ntiles ? uu : u) * 4096u + 1024u * (j & 3) + 16u * lane));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  uint32_t o0 = __builtin_nontemporal_load(off + t * 64u + lane), c0 = __builtin_nontemporal_load(cap + t * 64u + lane);
+  wl(t);
+  for (;;) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) *reinterpret_cast<v4u *>(g_lds + buf + 1024u * j + 16u * lane) = wv[j];
+    const uint32_t tn = t + 2 * nw;
+    if (tn < ntiles) wl(tn);
+    for (int h = 0; h < 2; h++) {
+      const uint32_t tt = t + h * nw;
+      if (tt < ntiles) {
+        const uint32_t x = fake_decode<SPIN>(buf + 4096u * h + 64u * lane + (o0 & 15u), o0, c0);
+        store_rec(rec, (uint64_t)tt * 64u + lane, x);
+      }
+    }
+    if (tn >= ntiles) break;
+    t = tn;
+    o0 = __builtin_nontemporal_load(off + t * 64u + lane);
+    c0 = __builtin_nontemporal_load(cap + t * 64u + lane);
+  }
+}
+
 // LDS-DMA with NB buffers per wave (NB - 1 tiles in flight); a tile's DMA: 4 x 1 KiB data + 2
 // descriptor loads = 6 VMEM instructions; the stores of a tile are issued after the next
 // tile's DMA.  Wait for tile k at the top of iteration k: the VMEM instructions issued after
@@ -187,7 +228,7 @@ static void run(int cus, const uint8_t *data, const uint32_t *off, const uint32_
   for (int wpc : {1, 2, 3, 4}) {
     const dim3 g(cus * wpc);
     rep("reg", wpc, timeit([&] { hipLaunchKernelGGL(reg_k<SPIN>, g, dim3(256), 4 * 4096, 0, data, off, cap, rec, ntiles); }, reps));
-    rep("regws", wpc, timeit([&] { hipLaunchKernelGGL((reg_k<SPIN, true>), g, dim3(256), 4 * 4096, 0, data, off, cap, rec, ntiles); }, reps));
+    rep("reg2", wpc, timeit([&] { hipLaunchKernelGGL(reg2_k<SPIN>, g, dim3(256), 4 * 8192, 0, data, off, cap, rec, ntiles); }, reps));
     rep("dma2", wpc, timeit([&] { hipLaunchKernelGGL((dma_k<2, SPIN>), g, dim3(256), 4 * 2 * 4608, 0, data, off, cap, rec, ntiles); }, reps));
     if (wpc <= 2) {
       rep("dma3", wpc, timeit([&] { hipLaunchKernelGGL((dma_k<3, SPIN>), g, dim3(256), 4 * 3 * 4608, 0, data, off, cap, rec, ntiles); }, reps));
@@ -215,9 +256,9 @@ int main(int argc, char **argv) {
   CK(hipMemset(cap, 0x40, n * 4u));
   CK(hipMalloc(&rec, n * 32u));
   run<0>(cus, data, off, cap, rec, ntiles, reps);
-  run<32>(cus, data, off, cap, rec, ntiles, reps);
   run<64>(cus, data, off, cap, rec, ntiles, reps);
   run<128>(cus, data, off, cap, rec, ntiles, reps);
+  run<192>(cus, data, off, cap, rec, ntiles, reps);
   CK(hipFree(data));
   CK(hipFree(off));
   CK(hipFree(cap));
