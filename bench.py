@@ -308,6 +308,16 @@ def attainable(n: int, read_bytes: int, local: int, achieved_gbps: float, soa: b
         if g2 is not None:
             out["record_form_probe"] = {"GBps": round(g2, 1), "probe_ms": round(ms2, 4),
                                         "of_attainable": round(achieved_gbps / g2, 4)}
+    # the read-only leg: the same loads with no stores — the measured ceiling the north star's
+    # "HBM-read roofline" target is judged against
+    g3, ms3 = probe(2)
+    if g3 is not None:
+        rg = ntiles * per_tile / (ms3 * 1e-3) / 1e9
+        ach_read = achieved_gbps * read_bytes / (read_bytes + n * 32)  # the launch's read share
+        out["read_only"] = {"GBps": round(rg, 1), "frac_of_peak": round(rg / HBM_PEAK_GBS, 4),
+                            "probe_ms": round(ms3, 4), "achieved_read_GBps": round(ach_read, 1),
+                            "of_read_ceiling": round(ach_read / rg, 4),
+                            "probe": "gpd_probe_stream2(soa=2): the same 16-B-per-lane nt loads, no stores"}
     return out
 
 

@@ -86,6 +86,30 @@ __global__ __launch_bounds__(256) void probe_soa_k(const v4u *__restrict__ in, u
   }
 }
 
+// Reads only (the north star's "HBM-read roofline" measured on the box): the same loads, no
+// result stores (one store per wave that never fires keeps the loads live).
+template <int MAXC>
+__global__ __launch_bounds__(256) void probe_read_k(const v4u *__restrict__ in, v4u *__restrict__ rec,
+                                                    uint32_t ntiles, uint32_t ctile) {
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint32_t nw = gridDim.x * 4u;
+  uint32_t x = 0;
+  for (uint32_t t = blockIdx.x * 4u + wave; t < ntiles; t += nw) {
+    const v4u *p = in + (uint64_t)t * ctile;
+    for (uint32_t c0 = 0; c0 < ctile; c0 += 64u * MAXC) {
+      v4u v[MAXC];
+#pragma unroll
+      for (int j = 0; j < MAXC; j++) {
+        const uint32_t c = c0 + 64u * j + lane;
+        v[j] = c < ctile ? __builtin_nontemporal_load(p + c) : v4u{0u, 0u, 0u, 0u};
+      }
+#pragma unroll
+      for (int j = 0; j < MAXC; j++) x ^= v[j].x + v[j].y + v[j].z + v[j].w;
+    }
+  }
+  if (x == 0x9E3779B9u) rec[blockIdx.x * 256u + threadIdx.x] = v4u{x, 0u, 0u, 0u};
+}
+
 }  // namespace
 
 extern "C" {
@@ -103,7 +127,7 @@ int gpd_probe_stream(int device, uint32_t ntiles, uint32_t read_bytes_per_tile, 
 }
 
 // gpd_probe_stream with the results stored as two 16-B records per lane (soa = 0, the gpd_record
-// form) or as the five SoA arrays (soa = 1).
+// form), as the five SoA arrays (soa = 1), or not at all (soa = 2: the read-only ceiling).
 int gpd_probe_stream2(int device, uint32_t ntiles, uint32_t read_bytes_per_tile, int reps, float warm_ms,
                       int soa, float *best_ms) {
   hipError_t e = hipSetDevice(device);
@@ -123,7 +147,10 @@ int gpd_probe_stream2(int device, uint32_t ntiles, uint32_t read_bytes_per_tile,
     const uint32_t g = (uint32_t)prop.multiProcessorCount * (uint32_t)wpc;
     const uint32_t pl = (ctile + 63u) / 64u;  // chunks per lane per tile
     auto launch = [&] {  // a 64-B-frame tile (4.5 KiB) in one round; longer tiles in rounds of 8 KiB
-      if (soa) {
+      if (soa == 2) {  // reads only
+        if (pl <= 5u) hipLaunchKernelGGL(probe_read_k<5>, dim3(g), dim3(256), 0, 0, in, rec, ntiles, ctile);
+        else hipLaunchKernelGGL(probe_read_k<8>, dim3(g), dim3(256), 0, 0, in, rec, ntiles, ctile);
+      } else if (soa) {
         uint8_t *r8 = reinterpret_cast<uint8_t *>(rec);
         if (pl <= 5u) hipLaunchKernelGGL(probe_soa_k<5>, dim3(g), dim3(256), 0, 0, in, r8, ntiles, ctile);
         else hipLaunchKernelGGL(probe_soa_k<8>, dim3(g), dim3(256), 0, 0, in, r8, ntiles, ctile);

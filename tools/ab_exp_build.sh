@@ -8,7 +8,7 @@ for N in "$@"; do
   D=ab_e$N
   rm -rf "$D"; mkdir -p "$D"
   tar --exclude=./.git --exclude=./gpurun_out --exclude=./profiles --exclude='./ab_*' \
-      --exclude='*.so' --exclude=__pycache__ -cf - . | tar -C "$D" -xf -
+      --exclude='*.so' --exclude=__pycache__ --exclude=./build -cf - . | tar -C "$D" -xf -
   (cd "$D" && GPD_EXTRA_CFLAGS="-DGPD_EXP=$N" python -c "from gopacket_amd.build import build_lib, build_synth, build_oracle; build_lib(force=True); build_synth(); build_oracle()")
   echo "built $D"
 done
