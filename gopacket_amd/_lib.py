@@ -42,7 +42,7 @@ class GpdResult(C.Structure):
 class GpdTuning(C.Structure):
     _fields_ = [("window_bytes", C.c_uint32), ("shift", C.c_int32), ("reg_prefix", C.c_int32),
                 ("waves_per_simd", C.c_int32), ("header_once", C.c_int32),
-                ("device_walk", C.c_int32), ("grid_rounds", C.c_int32)]
+                ("device_walk", C.c_int32), ("grid_rounds", C.c_int32), ("split", C.c_int32)]
 
 
 class GpdPcapInfo(C.Structure):

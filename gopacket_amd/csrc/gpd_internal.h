@@ -93,6 +93,7 @@ struct KParams {
   uint32_t fixed;              // tables in the kFix* layout (eth_mult shared by all three)
   uint32_t waves;              // fast kernel waves per SIMD (0: the default for the window)
   uint32_t rounds;             // fast kernel grid rounds of resident workgroups (0: the default)
+  uint32_t split;              // 4 KiB windows by the loader / decoder split kernel (sp_kernel)
   uint64_t *fb_list;           // fast kernel: packets left to the generic decoder (offset << 32 |
                                // index: the decode's loads skip the descriptor), in one private
                                // region per wave (64 x its tiles), which that wave decodes after

@@ -2465,6 +2465,212 @@ __global__ __launch_bounds__(256, MINW) void ro_kernel(KParams P) {
   decode_fallback_list<kRoStage / 64u, CS, HASH>(P, buf, fb_start, fb_c, lane, dlen, options);
 }
 
+// ---------------------------------------------------------------- loader / decoder split (round 6)
+// sp_kernel (gpd_tuning.split): 4 KiB windows of small frames with the two jobs of a wave split
+// between waves.  A workgroup is 8 waves: wave 0 only LOADS — each tile's 64 offsets and caplens
+// by LDS-DMA kSpAhead tiles ahead, then its window (planned from them) by LDS-DMA, a steady
+// kSpAhead + 1 windows in flight per workgroup — into a ring of kSpSlots slots; waves 1..7 only
+// DECODE, tile g of the workgroup by wave 1 + g mod 7, straight from its slot.  In LDS:
+// ready[s] = tile + 1 once the tile's window landed in slot s, freed[s] = the slot's use count once
+// its decoder is done with it.  Every wait is an explicit counted vmcnt (the loader's VMEM
+// instructions are all LDS-DMA, so the compiler inserts none) and every spin is capped (a capped
+// spin leaves the tile to the fallback list, never a wrong result or a hang).  Measured why
+// (tools/micro/stream_split.hip, profiles/r06/micro/): one loader per workgroup keeps the request
+// stream steady while the decode runs on seven waves, where the register loop's waves each
+// alternate a burst of loads with a stretch of decode.
+// A packet the tile's one window does not cover (the tile's bytes exceed 4 KiB) goes to the
+// decoder wave's fallback list, decoded after the barrier that ends the ring.
+constexpr int kSpWaves = 8;                                 // 1 loader + 7 decoders
+constexpr uint32_t kSpDec = kSpWaves - 1;
+constexpr uint32_t kSpSlots = 12;                           // ring slots per workgroup
+constexpr uint32_t kSpAhead = 3;                            // tiles in flight ahead of the oldest (6 deeper: slower)
+constexpr uint32_t kSpWin = 4096, kSpPad = 128;             // window, read-past pad
+constexpr uint32_t kSpDesc = kSpWin + kSpPad;               // 64 offsets + 64 caplens
+constexpr uint32_t kSpHdr = kSpDesc + 512;                  // {base, nbytes}
+constexpr uint32_t kSpSlotBytes = kSpHdr + 16;
+constexpr uint32_t kSpSpinCap = 1u << 22;
+__host__ __device__ constexpr uint32_t sp_lds_bytes() { return kSpSlots * kSpSlotBytes + 8u * kSpSlots + 16u; }
+static_assert(kSpSlots >= kSpAhead + 1u + kSpDec + 1u, "sp ring: in flight + decoding + one");
+
+// min / max over the 64 lanes without LDS (the loader's critical path): DPP row shifts within each
+// row of 16, then the row broadcasts, the result in lane 63
+__device__ __forceinline__ uint32_t dpp_min(uint32_t v) {
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)v, 0x111, 0xF, 0xF, false));  // row_shr:1
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)v, 0x112, 0xF, 0xF, false));  // row_shr:2
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)v, 0x114, 0xF, 0xF, false));  // row_shr:4
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)v, 0x118, 0xF, 0xF, false));  // row_shr:8
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)v, 0x142, 0xA, 0xF, false));  // row_bcast:15
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)v, 0x143, 0xC, 0xF, false));  // row_bcast:31
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+__device__ __forceinline__ uint32_t dpp_max(uint32_t v) {
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false));
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+__device__ __forceinline__ uint32_t *sp_word(uint32_t a) {
+  return static_cast<uint32_t *>(__builtin_assume_aligned(g_lds + a, 4));
+}
+__device__ __forceinline__ uint32_t sp_ld(uint32_t a) {  // (every lane reads the same word: uniform)
+  return __builtin_amdgcn_readfirstlane(__hip_atomic_load(sp_word(a), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+__device__ __forceinline__ void sp_st(uint32_t a, uint32_t v) {
+  __hip_atomic_store(sp_word(a), v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <bool CS, bool HASH>
+__global__ __launch_bounds__(64 * kSpWaves, 4) void sp_kernel(KParams P) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  for (uint32_t k = threadIdx.x; k < P.image_words; k += 64 * kSpWaves)
+    reinterpret_cast<uint32_t *>(g_lds)[k] = P.image[k];
+  const uint32_t img = (P.image_words * 4u + 15u) & ~15u;
+  const uint32_t ring = img, ready = ring + kSpSlots * kSpSlotBytes, freed = ready + 4u * kSpSlots;
+  const uint32_t abort = freed + 4u * kSpSlots;  // set by a loader whose slot wait hit the cap
+  if (threadIdx.x <= 2u * kSpSlots) *sp_word(ready + 4u * threadIdx.x) = 0u;
+  __syncthreads();
+  const uint32_t n = P.n_dev ? min((uint32_t)P.n, *P.n_dev) : (uint32_t)P.n;
+  const uint32_t ntiles = (n + 63u) >> 6;
+  const uint32_t nb = gridDim.x, b = blockIdx.x;
+  const uint32_t dlen = (uint32_t)P.data_len;
+  const uint32_t options = P.options & ~kDiagMask;
+  // this workgroup's tiles: t = b + g nb, g < G
+  const uint32_t q = ntiles / nb, r = ntiles % nb;
+  const uint32_t G = q + (b < r ? 1u : 0u);
+  auto slot_at = [&](uint32_t g) { return ring + (g % kSpSlots) * kSpSlotBytes; };
+  if (wave == 0u) {
+    __builtin_amdgcn_s_setprio(3);  // the loader is every decoder's critical path: it issues first
+    // ---- the loader.  Issue order per tile g: desc(g) (two DMAs), window(g) (four).  The window
+    // is planned from three scalar loads issued kSpAhead tiles earlier (the first packet's offset,
+    // the last packet's offset and caplen: packets in lane order, as batches are laid out; a
+    // packet outside the window goes to its decoder's fallback list), so the loader's vector
+    // memory stream holds only its DMAs and every wait on it is the counted one below.
+    typedef const __attribute__((address_space(4))) uint32_t *cu32;
+    const cu32 soff = reinterpret_cast<cu32>(reinterpret_cast<uintptr_t>(P.offset));
+    const cu32 scap = reinterpret_cast<cu32>(reinterpret_cast<uintptr_t>(P.caplen));
+    struct Plan {
+      uint32_t o0, ol, cl;
+    };
+    auto plan_load = [&](uint32_t g) -> Plan {  // (uniform: scalar loads)
+      const uint32_t t = b + g * nb, i0 = t * 64u, il = min(i0 + 63u, n - 1u);
+      return Plan{soff[i0], soff[il], scap[il]};
+    };
+    Plan pl[kSpAhead];
+#pragma unroll
+    for (uint32_t k = 0; k < kSpAhead; k++) pl[k] = k < G ? plan_load(k) : Plan{0, 0, 0};
+    uint32_t sig = 0;  // tiles signalled ready
+    bool stop = false;
+    // tile g's plan sits in pl[g mod kSpAhead] (the inner loop unrolled: no register moves, and each
+    // plan is read before the next prefetch into its registers is issued — scalar loads return out
+    // of order, so any wait on them is lgkmcnt(0))
+    for (uint32_t g0 = 0; g0 < G && !stop; g0 += kSpAhead) {
+#pragma unroll
+      for (uint32_t kk = 0; kk < kSpAhead; kk++) {
+        const uint32_t g = g0 + kk;
+        if (g >= G || stop) break;
+        const uint32_t s = slot_at(g), t = b + g * nb;
+        if (g >= kSpSlots) {  // the slot's previous tile must be decoded
+          const uint32_t need = g / kSpSlots;
+          if (sp_ld(freed + 4u * (g % kSpSlots)) < need) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // whatever landed goes out first
+            for (; sig < g; sig++)
+              if (lane == 0u) sp_st(ready + 4u * (sig % kSpSlots), sig + 1u);
+            uint32_t spins = 0;
+            while (sp_ld(freed + 4u * (g % kSpSlots)) < need && ++spins < kSpSpinCap) __builtin_amdgcn_s_sleep(1);
+            if (spins >= kSpSpinCap) {  // (never expected) stop loading: the decoders send every
+              if (lane == 0u) sp_st(abort, 1u);  // tile not signalled to the fallback list
+              stop = true;
+              break;
+            }
+          }
+        }
+        // plan: [base, base + nbytes), base the first packet rounded down to 16, to the last
+        // packet's end (at most 4 KiB)
+        const uint32_t o0 = min(pl[kk].o0, dlen), ol = min(pl[kk].ol, dlen), el = ol + min(pl[kk].cl, dlen - ol);
+        const uint32_t base = __builtin_amdgcn_readfirstlane(o0 & ~15u);
+        const uint32_t nbytes = __builtin_amdgcn_readfirstlane(el > base ? min((el - base + 15u) & ~15u, kSpWin) : 0u);
+        pl[kk] = g + kSpAhead < G ? plan_load(g + kSpAhead) : Plan{0, 0, 0};
+        if (lane == 0u) {
+          *sp_word(s + kSpHdr) = base;
+          *sp_word(s + kSpHdr + 4u) = nbytes;
+        }
+        const uint32_t ii = min(t * 64u + lane, n - 1u);  // (a lane past n loads entry n - 1)
+        glds4(P.offset, 4u * ii, s + kSpDesc);
+        glds4(P.caplen, 4u * ii, s + kSpDesc + 256u);
+        // a chunk past nbytes re-reads the window's first (inside the batch contract's readable
+        // bound, and never read by a decoder)
+        const uint8_t *src = P.data + base;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const uint32_t c = 1024u * j + 16u * lane;
+          glds16(src, c < nbytes ? c : 0u, s + 1024u * j, true);
+        }
+        // with kSpAhead + 1 tiles in flight, tiles <= g - kSpAhead have landed: tell their
+        // decoders (after a slot wait's flush they may have been told already)
+        if (g >= kSpAhead && sig + kSpAhead <= g) {
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 * kSpAhead) : "memory");
+          for (; sig + kSpAhead <= g; sig++)
+            if (lane == 0u) sp_st(ready + 4u * (sig % kSpSlots), sig + 1u);
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (; sig < G; sig++)
+      if (lane == 0u) sp_st(ready + 4u * (sig % kSpSlots), sig + 1u);
+  }
+  // ---- the decoders
+  const uint32_t d = wave - 1u;
+  uint32_t fb_c = 0, fb_start = 0, gdec = 0;
+  if (wave != 0u) {
+    const uint32_t qq = G / kSpDec, rr = G % kSpDec;
+    fb_start = 64u * (b * q + min(b, r) + d * qq + min(d, rr));  // tiles of earlier workgroups, then of earlier decoders
+    gdec = b * kSpDec + d;
+    const FastCtx F{P.eth_mult, ((uint32_t)GPD_LT_PAYLOAD << 8) | (reinterpret_cast<const uint8_t *>(g_lds)[GPD_LT_PAYLOAD]),
+                    (options & GPD_OPT_IGNORE_UNSUPPORTED) ? GPD_ST_OK : GPD_ST_UNSUPPORTED,
+                    reinterpret_cast<const uint8_t *>(g_lds)[GPD_LT_FRAGMENT]};
+    const uint32_t fits = kSpWin - 15u;
+    for (uint32_t g = d; g < G; g += kSpDec) {
+      const uint32_t s = slot_at(g), t = b + g * nb, i = t * 64u + lane;
+      uint32_t spins = 0;
+      while (sp_ld(ready + 4u * (g % kSpSlots)) != g + 1u && ++spins < kSpSpinCap) {
+        if ((spins & 15u) == 0u && sp_ld(abort)) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+      // (a capped spin or an aborted loader: the whole tile to the fallback list)
+      const bool ok = sp_ld(ready + 4u * (g % kSpSlots)) == g + 1u;
+      const uint32_t base = lds_u32(s + kSpHdr), nbytes = lds_u32(s + kSpHdr + 4u);
+      const uint32_t valid = i < n ? 1u : 0u;
+      const uint32_t off = valid ? min(lds_u32(s + kSpDesc + 4u * lane), dlen) : 0u;
+      const uint32_t end = valid ? off + min(lds_u32(s + kSpDesc + 256u + 4u * lane), dlen - off) : 0u;
+      const bool cov = ok && valid && off >= base && end - base <= nbytes && end - off <= fits;
+      uint32_t fb = valid && !cov ? 1u : 0u;
+      Out res{0, 0, 0, 0, 0, 0};
+      Seg sg{0, 0, 0};
+      // (AL: the windows are unshifted, so the aligned-chunk transport sum; -5 % against the plain
+      // decoder here, profiles/r06/micro/split_kernel_ab.txt)
+      if (cov && !fast_decode<CS, HASH, false, false, true>(s + (off - base), end - off, F, res, s, sg)) fb = 1;
+      if (lane == 0u) sp_st(freed + 4u * (g % kSpSlots), g / kSpSlots + 1u);  // (release: the reads above first)
+      const uint64_t m = __ballot(fb != 0);
+      if (m) {
+        if (fb) P.fb_list[fb_start + fb_c + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                               __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = ((uint64_t)off << 32) | i;
+        fb_c += (uint32_t)__popcll(m);
+      }
+      if (valid && !fb) store_out(P, i, res);
+    }
+  }
+  __syncthreads();  // the ring is idle: its slots stage the fallback rounds
+  if (wave != 0u) {
+    if (lane == 0u) P.fb_wcount[gdec] = fb_c;  // (gpd_last_launch_split's count)
+    decode_fallback_list<kSpWin / 64u, CS, HASH>(P, slot_at(d), fb_start, fb_c, lane, dlen, options);
+  }
+}
+
 template <int STAGE, bool FAST, bool EXT, bool PAGES, bool SWZ, int WAVES, bool CS = true,
           bool HASH = true, int MINW = 1>
 static hipError_t launch_t(const KParams &P, hipStream_t stream, int num_cus) {
@@ -2531,6 +2737,21 @@ static hipError_t launch_ro(KParams &P, hipStream_t stream, int num_cus) {
   return hipGetLastError();
 }
 
+// The loader / decoder split (sp_kernel): 8-wave workgroups, two per CU (LDS), one round of
+// them by default (gpd_tuning.grid_rounds more).
+template <bool CS, bool HASH>
+static hipError_t launch_sp(KParams &P, hipStream_t stream, int num_cus) {
+  const uint64_t ntiles = (P.n + 63) / 64;
+  const size_t lds = ((P.image_words * 4u + 15u) & ~15u) + (size_t)sp_lds_bytes() + 64;
+  const uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>((160u * 1024u) / lds, 2));
+  const uint64_t blocks = std::min<uint64_t>(ntiles, (uint64_t)num_cus * per_cu * (P.rounds ? P.rounds : 1u));
+  P.fb_waves = (uint32_t)blocks * kSpDec;
+  if (blocks == 0) return hipSuccess;
+  if (P.fb_waves > (uint32_t)num_cus * kMaxFastWavesPerCU) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((sp_kernel<CS, HASH>), dim3((unsigned)blocks), dim3(64 * kSpWaves), lds, stream, P);
+  return hipGetLastError();
+}
+
 template <bool CS, bool HASH>
 static hipError_t launch_fast(KParams &P, hipStream_t stream, int num_cus) {
   // One register budget per kernel (4 waves per SIMD for 4 KiB windows, 3 for 8 KiB windows
@@ -2549,6 +2770,9 @@ static hipError_t launch_fast(KParams &P, hipStream_t stream, int num_cus) {
       return launch_rs<8192, CS, HASH, 3, false, false, false, false, true>(P, stream, num_cus);
     }
   }
+  // (the split kernel writes gpd_records: with the five SoA arrays its seven decoders per
+  // workgroup ran 0.397 ms against the register loop's 0.319 on config 2, same box)
+  if (P.stage == 4096 && P.split && P.rec) return launch_sp<CS, HASH>(P, stream, num_cus);
   if (P.stage == 4096) return launch_rs<4096, CS, HASH, 4>(P, stream, num_cus);
   if (P.options & kHeaderOnce) return launch_rs<8192, CS, HASH, 3, false, true, true>(P, stream, num_cus);
   if (P.options & kRegPrefix) return launch_rs<8192, CS, HASH, 3>(P, stream, num_cus);

@@ -457,17 +457,17 @@ class DecodingLayerParser:
     # Engine tuning (gpd_ctx_set_tuning): staging choices that never change a result.
     # Keys: window_bytes (0 auto / 4096 / 8192), shift and reg_prefix (-1 auto / 0 / 1),
     # waves_per_simd (0 auto / 2 / 3 / 4), header_once (-1 auto / 0 / 1 windows / 2 rounds),
-    # device_walk (-1 auto / 0 / 1) and grid_rounds (0 auto / 1..8).
+    # device_walk (-1 auto / 0 / 1), grid_rounds (0 auto / 1..8) and split (-1 auto / 0 / 1).
     Tuning: Optional[dict] = None
 
     def _apply_tuning(self):
         from ._lib import GpdTuning
         t = dict(window_bytes=0, shift=-1, reg_prefix=-1, waves_per_simd=0, header_once=-1,
-                 device_walk=-1, grid_rounds=0)
+                 device_walk=-1, grid_rounds=0, split=-1)
         t.update(self.Tuning or {})
         g = GpdTuning(int(t["window_bytes"]), int(t["shift"]), int(t["reg_prefix"]),
                       int(t["waves_per_simd"]), int(t["header_once"]), int(t["device_walk"]),
-                      int(t["grid_rounds"]))
+                      int(t["grid_rounds"]), int(t["split"]))
         check(lib.gpd_ctx_set_tuning(self._ctx.h, C.byref(g)), "gpd_ctx_set_tuning")
         self._ctx.tuned = dict(self.Tuning) if self.Tuning else None
 
@@ -482,15 +482,17 @@ class DecodingLayerParser:
         check(lib.gpd_decode(self.ctx().h, C.byref(b), C.byref(r), C.c_void_p(stream.cuda_stream)),
               "gpd_decode")
 
-    def DecodeBatch(self, batch: PacketBatch, ext: bool = False, detail: bool = True) -> BatchResult:
+    def DecodeBatch(self, batch: PacketBatch, ext: bool = False, detail: bool = True,
+                    records: bool = False) -> BatchResult:
         """Decode every packet of a host batch on the GPU (H2D, kernel, D2H).  With detail (the
         default) res.err(i) carries the reference's exact text and res.decoded(i) any depth; the
         batch keeps the fast path, and only the failing / deep packets' 24-B records come back
         (a device gather: no extra transfer for a clean batch).  ext adds the layer records
-        (generic path)."""
+        (generic path); records selects the gpd_record result form on the device (the form the
+        loader / decoder split kernel writes for small frames)."""
         torch = _torch()
         db = DeviceBatch(batch, self.device)
-        dr = DeviceResult(batch.n, self.device, ext, detail=detail)
+        dr = DeviceResult(batch.n, self.device, ext, detail=detail, records=records)
         self.decode_device(db, dr)
         torch.cuda.synchronize(self.device)
         return dr.to_host()

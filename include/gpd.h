@@ -424,6 +424,9 @@ typedef struct gpd_tuning {
                                host first: -1 automatic (on), 0 off, 1 on */
   int32_t  grid_rounds; /* ABI 10: the fast kernel's grid in rounds of resident workgroups
                            (each wave takes every (grid waves)-th tile): 0 automatic, 1..8 */
+  int32_t  split;       /* ABI 10: 4 KiB windows (small frames) with gpd_result.records by the
+                           loader / decoder split kernel — one loading wave and seven decoding
+                           waves per workgroup over an LDS ring: -1 automatic (on), 0 off, 1 on */
 } gpd_tuning;
 int  gpd_ctx_set_tuning(gpd_ctx *ctx, const gpd_tuning *t);
 const char *gpd_last_error_string(void);

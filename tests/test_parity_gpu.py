@@ -102,6 +102,8 @@ def run_both(batch, first=L.LayerTypeEthernet, mask=ALL, options=0, tables=None,
         dev = p.DecodeBatch(batch, ext=e)
         assert_same(dev, ref, batch, e)
         out = out or dev
+        if not e:  # the gpd_record form too: small frames then take the split kernel (round 6)
+            assert_same(p.DecodeBatch(batch, records=True), ref, batch, False)
     return out  # the ext result when ext records were asked for
 
 
@@ -245,13 +247,14 @@ def test_register_prefix_both_ways(rpfx):
     run_both(PacketBatch.from_packets(_golden_packets() * 4, align=1), ext=False, tuning=t)
 
 
-@pytest.mark.parametrize("shift", [0, 1])
-def test_window_shift_both_ways(shift):
-    """The fast kernel copies windows into LDS either as they lie or shifted so that network
-    headers land 16-byte aligned (chosen per batch by mean frame size).  Force each copy
+@pytest.mark.parametrize("shift,split", [(0, 0), (1, 0), (-1, 1)], ids=["plain", "shifted", "split"])
+def test_window_shift_both_ways(shift, split):
+    """The register-staged kernel copies windows into LDS either as they lie or shifted so that
+    network headers land 16-byte aligned (chosen per batch by mean frame size); the loader /
+    decoder split kernel (4 KiB windows, round 6) lands them as they lie by LDS-DMA.  Force each
     (gpd_ctx_set_tuning) on batches of every layout: aligned, packed unaligned, shuffled,
     pcap-like (offsets = 8 mod 16), tagged, VXLAN, mutated and truncated frames."""
-    t = dict(shift=shift)
+    t = dict(shift=shift, split=split)
     pk = _golden_packets()
     run_both(PacketBatch.from_packets(pk), ext=False, tuning=t)
     run_both(PacketBatch.from_packets(pk * 3, align=1), ext=False, tuning=t)
@@ -268,10 +271,11 @@ def test_window_shift_both_ways(shift):
     run_both(NP.index(cap).batch, ext=False, tuning=t)
 
 
-@pytest.mark.parametrize("window", [4096, 8192])
-def test_window_sizes_both_ways(window):
-    """Both LDS window sizes on every synthetic mix and the mutated golden packets."""
-    t = dict(window_bytes=window)
+@pytest.mark.parametrize("window,split", [(4096, 0), (4096, 1), (8192, -1)])
+def test_window_sizes_both_ways(window, split):
+    """Both LDS window sizes (4 KiB by the register loop and by the split kernel) on every
+    synthetic mix and the mutated golden packets."""
+    t = dict(window_bytes=window, split=split)
     for maker in (synth.make_udp64, synth.make_imix, synth.make_vxlan, synth.make_mixed):
         run_both(maker(1 << 12), ext=False, tuning=t)
     run_both(PacketBatch.from_packets(_mutations(seed=29, per_packet=20)), ext=False, tuning=t)
@@ -495,19 +499,21 @@ def test_vxlan_frame_shapes_in_every_kernel(align):
 
 
 @pytest.mark.parametrize("geom", [dict(waves_per_simd=2, grid_rounds=1), dict(waves_per_simd=3, grid_rounds=2),
-                                  dict(waves_per_simd=4, grid_rounds=8), dict(grid_rounds=1)],
-                         ids=["w2r1", "w3r2", "w4r8", "r1"])
+                                  dict(waves_per_simd=4, grid_rounds=8), dict(grid_rounds=1), dict(split=1),
+                                  dict(split=1, grid_rounds=3), dict(split=0), dict(split=0, grid_rounds=1)],
+                         ids=["w2r1", "w3r2", "w4r8", "r1", "split", "split_r3", "nosplit", "nosplit_r1"])
 def test_launch_geometry_never_changes_results(geom):
     """gpd_tuning.waves_per_simd (now enforced: an LDS reservation of 1/W of the CU per
-    workgroup) and grid_rounds (ABI 10) change only how many waves stream and how many tiles
-    each takes, through every fast kernel (4 KiB windows shifted, 8 KiB AL / plain / header-once
-    windows, rounds) with fallback lists, against the oracle; with more tiles than one round of
-    waves and with fewer."""
+    workgroup), grid_rounds and split (ABI 10) change only how many waves stream and how many
+    tiles each takes, through every fast kernel (4 KiB windows shifted, 8 KiB AL / plain /
+    header-once windows, rounds, the loader / decoder split over an LDS ring) with fallback
+    lists, against the oracle; with more tiles than one round of waves and with fewer, and 4 KiB
+    windows too small for a tile's bytes (the split kernel lists the uncovered packets)."""
     mixed = synth.make_mixed(6000)
     golden = PacketBatch.from_packets(_golden_packets() * 7)
     cases = [(synth.make_udp64(40000), {}), (synth.make_vxlan(20000), {}), (synth.make_imix(12000), {}),
-             (mixed, {}), (mixed, dict(window_bytes=8192, header_once=1)),
-             (golden, dict(window_bytes=4096)), (synth.make_udp64(3000), {})]
+             (mixed, {}), (mixed, dict(window_bytes=8192, header_once=1)), (mixed, dict(window_bytes=4096)),
+             (golden, dict(window_bytes=4096)), (synth.make_udp64(3000), {}), (synth.make_udp64(70), {})]
     for b, t in cases:
         run_both(b, ext=False, tuning=dict(t, **geom))
 

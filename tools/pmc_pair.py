@@ -9,7 +9,7 @@ for d in sys.argv[1:]:
     acc = collections.defaultdict(lambda: collections.defaultdict(float))
     for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            if not any(k in r["Kernel_Name"] for k in ("rs_kernel", "ro_kernel", "decode_kernel")):
+            if not any(k in r["Kernel_Name"] for k in ("rs_kernel", "ro_kernel", "decode_kernel", "sp_kernel")):
                 continue
             acc[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
     ks = list(acc.values())
