@@ -179,7 +179,7 @@ def load_traffic(config: str):
         s = json.load(open(paths[-1]))
     except (OSError, ValueError):
         return None
-    k = [v for n, v in s.get("kernels", {}).items() if "decode_kernel" in n or "rs_kernel" in n or "ro_kernel" in n]
+    k = [v for n, v in s.get("kernels", {}).items() if "decode_kernel" in n or "rs_kernel" in n or "ro_kernel" in n or "sp_kernel" in n]
     return {"read": s.get("hbm_read_bytes_per_launch"), "write": s.get("hbm_write_bytes_per_launch"),
             "kernel_us": k[0]["avg_us"] if k else None,
             "source": os.path.relpath(paths[-1], ROOT)}

@@ -27,7 +27,7 @@ def per_stream(d):
     for f in glob.glob(os.path.join(d, "kt", "**", "*kernel_trace.csv"), recursive=True):
         g = collections.defaultdict(list)
         for r in csv.DictReader(open(f)):
-            if any(k in r["Kernel_Name"] for k in ("rs_kernel", "ro_kernel", "decode_kernel")):
+            if any(k in r["Kernel_Name"] for k in ("rs_kernel", "ro_kernel", "sp_kernel", "decode_kernel")):
                 g[r["Stream_Id"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
         for k, v in g.items():
             out["stream_" + k] = {"calls": len(v), "avg_us": sum(v) / len(v), "min_us": min(v),
@@ -40,7 +40,7 @@ def counters(d, name):
     meta = {}
     for f in glob.glob(os.path.join(d, name, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if any(k in r["Kernel_Name"] for k in ("rs_kernel", "ro_kernel", "decode_kernel")):
+            if any(k in r["Kernel_Name"] for k in ("rs_kernel", "ro_kernel", "sp_kernel", "decode_kernel")):
                 acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
                 meta = {k: r[k] for k in ("Kernel_Name", "Grid_Size", "Workgroup_Size",
                                           "LDS_Block_Size", "VGPR_Count", "SGPR_Count",
@@ -66,7 +66,7 @@ def summarize(d):
     clk, _ = counters(d, "clk")
     if clk:
         s["clk_per_launch"] = clk
-        dec = [v for k, v in s["kernels"].items() if any(x in k for x in ("rs_kernel", "ro_kernel", "decode_kernel"))]
+        dec = [v for k, v in s["kernels"].items() if any(x in k for x in ("rs_kernel", "ro_kernel", "sp_kernel", "decode_kernel"))]
         if dec and "GRBM_GUI_ACTIVE" in clk:  # the decode kernel's mean time from the kt pass
             us = max(dec, key=lambda v: v["calls"])["avg_us"]
             s["effective_clock_ghz"] = clk["GRBM_GUI_ACTIVE"] / 8 / (us * 1e3)
