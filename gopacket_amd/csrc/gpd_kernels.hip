@@ -2539,9 +2539,14 @@ __global__ __launch_bounds__(64 * kSpWaves, 4) void sp_kernel(KParams P) {
   const uint32_t nb = gridDim.x, b = blockIdx.x;
   const uint32_t dlen = (uint32_t)P.data_len;
   const uint32_t options = P.options & ~kDiagMask;
-  // this workgroup's tiles: t = b + g nb, g < G
+  // this workgroup's tiles: one contiguous run, t = c0 + g, g < G.  (Against the grid-strided
+  // order t = b + g nb, where the whole grid reads one 2-MiB stretch at a time: faster in 71 of
+  // 80 (box, buffer placement) pairs, by 1-3 %, at most 1 % slower in the rest;
+  // tools/mode_probe.py, DESIGN.md §5 sp_kernel.)
   const uint32_t q = ntiles / nb, r = ntiles % nb;
   const uint32_t G = q + (b < r ? 1u : 0u);
+  const uint32_t c0 = b * q + min(b, r);
+  auto tile_of = [&](uint32_t g) { return c0 + g; };
   auto slot_at = [&](uint32_t g) { return ring + (g % kSpSlots) * kSpSlotBytes; };
   if (wave == 0u) {
     __builtin_amdgcn_s_setprio(3);  // the loader is every decoder's critical path: it issues first
@@ -2557,7 +2562,7 @@ __global__ __launch_bounds__(64 * kSpWaves, 4) void sp_kernel(KParams P) {
       uint32_t o0, ol, cl;
     };
     auto plan_load = [&](uint32_t g) -> Plan {  // (uniform: scalar loads)
-      const uint32_t t = b + g * nb, i0 = t * 64u, il = min(i0 + 63u, n - 1u);
+      const uint32_t t = tile_of(g), i0 = t * 64u, il = min(i0 + 63u, n - 1u);
       return Plan{soff[i0], soff[il], scap[il]};
     };
     Plan pl[kSpAhead];
@@ -2573,7 +2578,7 @@ __global__ __launch_bounds__(64 * kSpWaves, 4) void sp_kernel(KParams P) {
       for (uint32_t kk = 0; kk < kSpAhead; kk++) {
         const uint32_t g = g0 + kk;
         if (g >= G || stop) break;
-        const uint32_t s = slot_at(g), t = b + g * nb;
+        const uint32_t s = slot_at(g), t = tile_of(g);
         if (g >= kSpSlots) {  // the slot's previous tile must be decoded
           const uint32_t need = g / kSpSlots;
           if (sp_ld(freed + 4u * (g % kSpSlots)) < need) {
@@ -2635,7 +2640,7 @@ __global__ __launch_bounds__(64 * kSpWaves, 4) void sp_kernel(KParams P) {
                     reinterpret_cast<const uint8_t *>(g_lds)[GPD_LT_FRAGMENT]};
     const uint32_t fits = kSpWin - 15u;
     for (uint32_t g = d; g < G; g += kSpDec) {
-      const uint32_t s = slot_at(g), t = b + g * nb, i = t * 64u + lane;
+      const uint32_t s = slot_at(g), t = tile_of(g), i = t * 64u + lane;
       uint32_t spins = 0;
       while (sp_ld(ready + 4u * (g % kSpSlots)) != g + 1u && ++spins < kSpSpinCap) {
         if ((spins & 15u) == 0u && sp_ld(abort)) break;
