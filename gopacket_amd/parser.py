@@ -311,8 +311,17 @@ class DeviceBatch:
         self.n = batch.n
         self.data_len = batch.data_len
         self.data = torch.from_numpy(batch.data).to(dev)
-        self.offset = torch.from_numpy(batch.offset.view(np.int32)).to(dev)
-        self.caplen = torch.from_numpy(batch.caplen.view(np.int32)).to(dev)
+        # offset[] and caplen[] share one allocation, caplen[] right after offset[]: the two
+        # descriptor streams are read in lock-step, and their relative placement in HBM moves
+        # the 4 KiB kernels by 4-5 % (DESIGN §5a "Tile order and descriptor placement");
+        # adjacent halves of one allocation measured fast at every address tried.  caplen[]
+        # starts on a 64-B boundary (no gap when n is a multiple of 16).
+        n, pad = self.n, (-self.n) % 16
+        host = np.zeros(2 * n + pad, dtype=np.int32)
+        host[:n] = batch.offset.view(np.int32)
+        host[n + pad:] = batch.caplen.view(np.int32)
+        desc = torch.from_numpy(host).to(dev)
+        self.offset, self.caplen = desc[:n], desc[n + pad:]
         self.device = device
 
     def c_batch(self) -> GpdBatch:

@@ -63,6 +63,8 @@ def main():
             db, dr = dbs[t // trials], drs[t % trials]
         else:
             db = P.DeviceBatch(batch, 0)
+            if os.environ.get("MODE_ALT") == "1" and t % 2:  # odd trials: separate offset / caplen allocations (the pre-r06 layout)
+                db.offset, db.caplen = db.offset.clone(), db.caplen.clone()
             dr = P.DeviceResult(n, 0, ext=False, hdr_off=False, records=True)
             keep.append((db, dr))
         for tu in tunes:
@@ -78,7 +80,7 @@ def main():
                 torch.cuda.synchronize(0)
                 ms.append(round(e0.elapsed_time(e1) / 50, 4))
             st = dr.records.view(torch.int32)[0::8].cpu().numpy()
-            print(json.dumps({"trial": t, "tune": tu, "ms": ms, "errors": int(((st & 3) != 0).sum()),
+            print(json.dumps({"trial": t, "tune": tu, "layout": "separate" if int(db.caplen.data_ptr()) - int(db.offset.data_ptr()) != 4 * n else "packed", "ms": ms, "errors": int(((st & 3) != 0).sum()),
                               "data": hex(db.data.data_ptr()), "off": hex(db.offset.data_ptr()), "cap": hex(db.caplen.data_ptr()), "rec": hex(dr.records.data_ptr())}),
                   flush=True)
 
