@@ -2561,8 +2561,14 @@ __global__ __launch_bounds__(64 * kSpWaves, 4) void sp_kernel(KParams P) {
     struct Plan {
       uint32_t o0, ol, cl;
     };
+    // Each scalar plan load fetches its own 128-B line from HBM, which the descriptor DMA then
+    // fetches again (profiles/r06/micro/desc_plan_ab/).  When the batch averages >= 63 bytes per
+    // packet a tile's packets span ~4 KiB anyway: the window is then always 4 KiB (capped at the
+    // batch end) and one load, the first packet's offset, plans it.
+    const bool fixedw = (uint64_t)dlen >= 63ull * n;
     auto plan_load = [&](uint32_t g) -> Plan {  // (uniform: scalar loads)
       const uint32_t t = tile_of(g), i0 = t * 64u, il = min(i0 + 63u, n - 1u);
+      if (fixedw) return Plan{soff[i0], 0u, 0u};
       return Plan{soff[i0], soff[il], scap[il]};
     };
     Plan pl[kSpAhead];
@@ -2598,7 +2604,8 @@ __global__ __launch_bounds__(64 * kSpWaves, 4) void sp_kernel(KParams P) {
         // packet's end (at most 4 KiB)
         const uint32_t o0 = min(pl[kk].o0, dlen), ol = min(pl[kk].ol, dlen), el = ol + min(pl[kk].cl, dlen - ol);
         const uint32_t base = __builtin_amdgcn_readfirstlane(o0 & ~15u);
-        const uint32_t nbytes = __builtin_amdgcn_readfirstlane(el > base ? min((el - base + 15u) & ~15u, kSpWin) : 0u);
+        const uint32_t nbytes = __builtin_amdgcn_readfirstlane(
+            fixedw ? min((dlen - base + 15u) & ~15u, kSpWin) : el > base ? min((el - base + 15u) & ~15u, kSpWin) : 0u);
         pl[kk] = g + kSpAhead < G ? plan_load(g + kSpAhead) : Plan{0, 0, 0};
         if (lane == 0u) {
           *sp_word(s + kSpHdr) = base;

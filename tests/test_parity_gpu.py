@@ -281,6 +281,25 @@ def test_window_sizes_both_ways(window, split):
     run_both(PacketBatch.from_packets(_mutations(seed=29, per_packet=20)), ext=False, tuning=t)
 
 
+@pytest.mark.parametrize("lo,hi", [(44, 76), (48, 80), (60, 68)], ids=["mean60", "mean64", "mean64_narrow"])
+def test_split_kernel_window_plans(lo, hi):
+    """The split kernel plans each tile's window from its first packet's offset alone (always
+    4 KiB, capped at the batch end) when the batch averages >= 63 bytes per packet, else from the
+    first offset and the last packet's end.  Packed frames of random length around 64 bytes: tiles
+    shorter than 4 KiB (over-read window), longer (packets past the window take the fallback
+    list) and the batch's last, partial tile, on both sides of the threshold."""
+    rng = np.random.default_rng(lo * 1000 + hi)
+    base = synth.make_udp64(3000)
+    pk = []
+    for i in range(base.n):
+        p = base.packet(i)
+        k = int(rng.integers(lo, hi + 1))
+        pk.append(p[:k] if k <= len(p) else p + bytes(k - len(p)))
+    b = PacketBatch.from_packets(pk, align=1)
+    assert (b.data_len >= 63 * b.n) == (lo + hi >= 2 * 63)
+    run_both(b, ext=False, tuning=dict(window_bytes=4096, split=1))
+
+
 @pytest.mark.parametrize("extra", [{}, {"reg_prefix": 0}, {"shift": 1}, {"waves_per_simd": 2}],
                          ids=["default", "lds_prefix", "shifted", "two_waves"])
 @pytest.mark.parametrize("ho", [0, 1, 2])
